@@ -1,0 +1,292 @@
+"""Benchmark: reactions/s of the CGR-MPNN-3D training step on 1..8 MI355X (one process per GPU).
+
+    python bench.py [--gpus N --steps K --warmup W]                      (N = 1)
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W          (N > 1, RCCL)
+
+A step is one pass of the hot path over one synthetic, HBM-resident batch of BASELINE config 2
+(256 reactions per GPU, 30 atoms / 60 directed edges each, F = 846, Fe = 14, depth 4, hidden
+400): forward, MSELoss(sum), backward (native), RCCL all-reduce(SUM) of the flat gradient
+bucket when N > 1, Adam(amsgrad) step (train.py:117-121).  Per-GPU work is fixed (weak scaling).
+Rank 0 prints ONE JSON line.  See DESIGN.md "Measurement".
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "cgr-mpnn-3d_amd"))
+sys.path.insert(0, REPO)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "reactions/sec (fwd+bwd) depth=4 hidden=400 T1x batch; 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="cfg2", choices=["cfg1", "cfg2", "cfg4", "cfg5"])
+    ap.add_argument("--graph", type=int, default=-1,
+                    help="capture the step in a HIP graph (1/0; -1 = auto: on for N = 1)")
+    ap.add_argument("--cpu-baseline", type=int, default=1)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--profile-steps", type=int, default=10,
+                    help="instrumented steps (HIP events per kernel class) after the timed run")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------------------------------------------
+# algorithmic work per kernel class and step (DESIGN.md "Roofline accounting")
+# ------------------------------------------------------------------------------------------------
+def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
+    f4 = 4
+    pre = 0 if relu else 1
+    w = {}
+    w["gemm_nt_layer_fwd"] = dict(
+        flops=D * 2.0 * E * H * H,
+        bytes=D * f4 * (N * H + E * H + E * H + E * H * (1 + pre) + H * H) + D * 8.0 * E)
+    w["gemm_nt_node_P"] = dict(flops=2.0 * N * F * H, bytes=f4 * (N * F + H * F + N * H))
+    w["gemm_nt_readout_fwd"] = dict(flops=2.0 * N * (F + H) * H,
+                                    bytes=f4 * (N * F + N * H + H * (F + H) + N * H * (1 + pre)))
+    w["gemm_nt_bwd"] = dict(flops=D * 2.0 * E * H * H + 2.0 * N * H * H,
+                            bytes=f4 * (D * (2 * E * H + H * H) + 2 * N * H + H * H))
+    tn_flops = 2.0 * N * H * (F + H) + D * 2.0 * E * H * H + 2.0 * E * H * Fe + 2.0 * N * H * F
+    tn_bytes = f4 * (N * H + N * (F + H) + D * (E * H + N * H + E * H) + E * H + E * Fe
+                     + N * H + N * F)
+    w["gemm_tn_wgrad"] = dict(flops=tn_flops, bytes=tn_bytes)
+    # scatter-add (segmented sum over dst CSR): read E rows, write N rows, + indices
+    seg = f4 * (E * H + N * H) + 4.0 * (N + 1)
+    w["segsum_dst_fwd"] = dict(flops=float((D + 1) * E * H), bytes=(D + 1) * seg)
+    w["segsum_src_bwd"] = dict(flops=float((D + 1) * E * H),
+                               bytes=(D + 1) * (seg + 4.0 * E))
+    w["layer_act_bwd"] = dict(flops=0.0, bytes=D * f4 * (E * H * 5 + N * H))
+    return w
+
+
+def mfma_bound(name):
+    return name.startswith("gemm")
+
+
+def roofline_entry(name, work, ms_per_step, traffic):
+    t = ms_per_step * 1e-3
+    if mfma_bound(name):
+        ach = work["flops"] / t / 1e12
+        peak = FP32_MFMA_PEAK_TFLOPS
+        unit = "TFLOP/s"
+    else:
+        ach = work["bytes"] / t / 1e9
+        peak = HBM_PEAK_GBS
+        unit = "GB/s"
+    return {"kernel": name, "bound": "mfma" if mfma_bound(name) else "hbm",
+            "achieved": round(ach, 3), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+            "traffic": traffic, "algorithmic_bytes": work["bytes"],
+            "algorithmic_flops": work["flops"], "ms_per_step": round(ms_per_step, 5)}
+
+
+# ------------------------------------------------------------------------------------------------
+def cpu_baseline(cfgname, seconds):
+    """Reference CPU path (oracle/dmpnn_torch.py: the reference ATen op sequence incl. its dead
+    readout GEMM) on this host's cores: same batch shape, MSE(sum) + backward + Adam(amsgrad)."""
+    from cgr_mpnn_3D._amd.synth import CONFIGS, make_batch
+    from oracle.dmpnn_torch import TorchRestatement, random_state_dict
+
+    c = CONFIGS[cfgname]
+    b = make_batch(c["num_graphs"], c["n_atoms"], c["n_bonds"], c["n_mace"], seed=1234)
+    F_ = b.x.shape[1]
+    sd = random_state_dict(F_, 14, c["hidden"], c["depth"], c["learnable_skip"], seed=0)
+    m = TorchRestatement(sd, c["depth"], learnable_skip=c["learnable_skip"])
+    m.train()
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, amsgrad=True)
+    x = torch.from_numpy(b.x)
+    ei = torch.from_numpy(b.edge_index)
+    ea = torch.from_numpy(b.edge_attr)
+    bt = torch.from_numpy(b.batch)
+    y = torch.from_numpy(b.y)
+    loss_fn = torch.nn.MSELoss(reduction="sum")
+
+    def step():
+        opt.zero_grad()
+        loss = loss_fn(m(x, ei, ea, bt, b.num_graphs), y)
+        loss.backward()
+        opt.step()
+
+    for _ in range(2):
+        step()
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        step()
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or n >= 200:
+            break
+    return {"value": round(n * b.num_graphs / el, 2), "unit": "reactions/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"{n} training steps of the {cfgname} batch ({b.num_graphs} reactions, "
+                      f"fwd+MSE+bwd+Adam) with the torch-CPU restatement of the reference op "
+                      f"sequence, {el:.1f} s, torch {torch.__version__}, "
+                      f"{torch.get_num_threads()} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.graph < 0:
+        args.graph = 1 if world == 1 else 0
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from cgr_mpnn_3D._amd import native
+    from cgr_mpnn_3D._amd.ddp import install_grad_allreduce
+    from cgr_mpnn_3D._amd.synth import CONFIGS, make_batch
+    from cgr_mpnn_3D.models.GNN import GNN
+
+    c = CONFIGS[args.config]
+    D, H = c["depth"], c["hidden"]
+    b = make_batch(c["num_graphs"], c["n_atoms"], c["n_bonds"], c["n_mace"], seed=1234 + rank)
+    data = b.to_torch(dev)
+    N, E, B = b.x.shape[0], b.edge_index.shape[1], b.num_graphs
+    F_ = b.x.shape[1]
+    torch.manual_seed(0)
+    model = GNN(F_, 14, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D,
+                use_learnable_skip=c["learnable_skip"]).to(dev)
+    model.train()
+    if world > 1:
+        install_grad_allreduce(model)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3, amsgrad=True, capturable=bool(args.graph))
+    loss_fn = torch.nn.MSELoss(reduction="sum")
+
+    def step():
+        opt.zero_grad(set_to_none=False)
+        loss = loss_fn(model(data), data.y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    # warmup (eager), then optional graph capture of the whole step
+    log(f"[bench] rank {rank}/{world} {args.config}: N={N} E={E} B={B} F={F_} H={H} D={D}")
+    for _ in range(max(3, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    run = step
+    if args.graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        run = g.replay
+        for _ in range(args.warmup):
+            run()
+        torch.cuda.synchronize()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        run()
+        if rank == 0 and (i + 1) % max(1, args.steps // 5) == 0:
+            log(f"[bench] step {i + 1}/{args.steps}")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el / args.steps * 1e3
+    value = world * B * args.steps / el
+
+    # per-kernel-class device time with HIP events on the launch stream (eager, instrumented)
+    lib = native.load()
+    roof = None
+    roof_scatter = None
+    breakdown = {}
+    if args.profile_steps > 0:
+        lib.cgr_profile_reset()
+        lib.cgr_profile_enable(1)
+        for _ in range(args.profile_steps):
+            step()
+        torch.cuda.synchronize()
+        lib.cgr_profile_enable(0)
+        rep = native.profile_report()
+        work = algorithmic_work(N, E, B, F_, 14, H, D)
+        traffic = {}
+        if os.path.exists(args.traffic_json):
+            try:
+                traffic = json.load(open(args.traffic_json)).get(args.config, {})
+            except Exception:  # noqa: BLE001
+                traffic = {}
+        for name, (cnt, tot) in rep.items():
+            breakdown[name] = {"launches_per_step": cnt / args.profile_steps,
+                               "ms_per_step": round(tot / args.profile_steps, 5)}
+        cands = [k for k in rep if k in work]
+        if cands:
+            dom = max(cands, key=lambda k: rep[k][1])
+            roof = roofline_entry(dom, work[dom], rep[dom][1] / args.profile_steps,
+                                  traffic.get(dom))
+        if "segsum_dst_fwd" in rep:
+            roof_scatter = roofline_entry("segsum_dst_fwd", work["segsum_dst_fwd"],
+                                          rep["segsum_dst_fwd"][1] / args.profile_steps,
+                                          traffic.get("segsum_dst_fwd"))
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        log("[bench] timing the CPU baseline (reference op sequence, torch CPU) ...")
+        cpu = cpu_baseline(args.config, args.cpu_seconds)
+
+    if rank == 0:
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "reactions/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic T1x-shaped batches (seeded generator, HBM-resident), random-init "
+                    "weights",
+            "config": {
+                "workload": f"{args.config}: CGR-MPNN-3D depth={D} hidden={H}, {B} reactions/GPU "
+                            f"({c['n_atoms']} atoms, {2 * c['n_bonds']} directed edges each), "
+                            f"F={F_} (78 CGR + {c['n_mace']} MACE), Fe=14, ReLU, dropout 0; step "
+                            f"= fwd + MSELoss(sum) + bwd + grad all-reduce (N>1) + "
+                            f"Adam(amsgrad)" + (", HIP-graph captured" if args.graph else ""),
+                "global_batch": world * B, "parallelism": f"dp{world}"},
+            "roofline": roof, "roofline_scatter_add": roof_scatter, "kernel_breakdown": breakdown,
+            "cpu_baseline": cpu,
+        }
+        if cpu:
+            out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,125 @@
+"""autograd bridge: ``GNN.forward`` / backward -> ``cgr_gnn_forward`` / ``cgr_gnn_backward``.
+
+The whole model step is ONE native call each way (≈25 kernel launches enqueued from C++), so the
+host cost per training step is two ctypes calls plus a few caching-allocator allocations; every
+launch goes to ``torch.cuda.current_stream()`` and nothing synchronises, so a training step can be
+captured into a CUDA/HIP graph.
+"""
+
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_float, c_void_p
+
+import torch
+
+from . import config as _config
+from . import native
+
+
+def make_config(num_node_features, num_edge_features, hidden, depth, act_code, learnable_skip):
+    return native.CgrGnnConfig(int(num_node_features), int(num_edge_features), int(hidden),
+                               int(depth), int(act_code), 1 if learnable_skip else 0)
+
+
+def _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, num_graphs):
+    return native.CgrBatch(
+        native.ptr(x), native.ptr(edge_index),
+        native.ptr(edge_attr) if edge_attr is not None and edge_attr.numel() else None,
+        native.ptr(batch), native.ptr(graph_ptr),
+        int(x.shape[0]), int(edge_index.shape[1]), int(num_graphs))
+
+
+def _param_table(tensors):
+    arr = (c_void_p * len(tensors))()
+    for i, t in enumerate(tensors):
+        arr[i] = t.data_ptr()
+    return arr
+
+
+def _dropout_array(dropout_ps, depth):
+    if dropout_ps is None:
+        return None
+    arr = (c_float * depth)()
+    for i in range(depth):
+        arr[i] = float(dropout_ps[i])
+    return arr
+
+
+def read_status(arena, cfg, N, E, B) -> int:
+    """Graph-prep status word (bit0 bad edge index, bit1 bad/unsorted batch).  Synchronises."""
+    lib = native.load()
+    off = lib.cgr_gnn_arena_offset(ctypes.byref(cfg), N, E, B, b"status", 0)
+    return int(arena[off:off + 4].view(torch.int32).item())
+
+
+class GNNFunction(torch.autograd.Function):
+    """y[B] = GNN(x, edge_index, edge_attr, batch; params) on the MI355X path."""
+
+    @staticmethod
+    def forward(ctx, cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs,
+                dropout_ps, seed, training, bucket_hook, *params):
+        lib = native.load()
+        cfg = make_config(*cfg_tuple)
+        N, E, B = int(x.shape[0]), int(edge_index.shape[1]), int(num_graphs)
+        dev = x.device
+        arena_bytes = lib.cgr_gnn_arena_bytes(ctypes.byref(cfg), N, E, B)
+        if arena_bytes < 0:
+            native.check(1)
+        arena = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
+        y = torch.empty(B, dtype=torch.float32, device=dev)
+        bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
+        ptab = _param_table(params)
+        dps = _dropout_array(dropout_ps, cfg.depth)
+        native.check(lib.cgr_gnn_forward(ctypes.byref(cfg), ptab, ctypes.byref(bs), dps,
+                                         ctypes.c_uint64(seed), int(bool(training)), native.ptr(arena),
+                                         native.ptr(y), native.stream_ptr(dev)))
+        if _config.strict:
+            st = read_status(arena, cfg, N, E, B)
+            if st & 1:
+                raise IndexError("cgr_mpnn_3D: edge_index holds a node id outside [0, num_nodes)")
+            if st & 2:
+                raise RuntimeError("cgr_mpnn_3D: batch vector is not sorted / out of range")
+        ctx.cfg_tuple = cfg_tuple
+        ctx.num_graphs = B
+        ctx.dropout_ps = dropout_ps
+        ctx.seed = seed
+        ctx.training = training
+        ctx.bucket_hook = bucket_hook
+        ctx.save_for_backward(x, edge_index, edge_attr, batch, graph_ptr, arena, *params)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        lib = native.load()
+        x, edge_index, edge_attr, batch, graph_ptr, arena, *params = ctx.saved_tensors
+        cfg = make_config(*ctx.cfg_tuple)
+        N, E, B = int(x.shape[0]), int(edge_index.shape[1]), ctx.num_graphs
+        dev = x.device
+        ws = torch.empty(lib.cgr_gnn_workspace_bytes(ctypes.byref(cfg), N, E, B),
+                         dtype=torch.uint8, device=dev)
+        # one flat gradient bucket (ready for a single all-reduce), viewed per parameter
+        numels = [p.numel() for p in params]
+        flat = torch.empty(sum(numels), dtype=torch.float32, device=dev)
+        grads = []
+        off = 0
+        for p, n in zip(params, numels):
+            grads.append(flat[off:off + n].view(p.shape))
+            off += n
+        dy = dy.contiguous().float()
+        bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
+        native.check(lib.cgr_gnn_backward(
+            ctypes.byref(cfg), _param_table(params), ctypes.byref(bs),
+            _dropout_array(ctx.dropout_ps, cfg.depth), ctypes.c_uint64(ctx.seed),
+            int(bool(ctx.training)), native.ptr(arena), native.ptr(dy), _param_table(grads),
+            native.ptr(ws), native.stream_ptr(dev)))
+        hook = ctx.bucket_hook if ctx.bucket_hook is not None else _config.grad_bucket_hook
+        if hook is not None:
+            hook(flat)  # e.g. RCCL all-reduce of the whole bucket (cgr_mpnn_3D._amd.ddp)
+        return (None,) * 11 + tuple(grads)
+
+
+def gnn_forward(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, dropout_ps,
+                seed, training, params, bucket_hook=None):
+    return GNNFunction.apply(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs,
+                             dropout_ps, seed, training, bucket_hook, *params)

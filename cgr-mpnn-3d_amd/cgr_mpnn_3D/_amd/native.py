@@ -1,0 +1,135 @@
+"""ctypes binding of ``libcgr_mpnn3d.so`` (the C ABI declared in ``include/cgr_mpnn3d.h``).
+
+There is deliberately no fallback: if the shared library is missing or fails to load, every
+model call raises.  The library is built in-tree by ``__graft_entry__.build()`` /
+``make -C cgr-mpnn-3d_amd/csrc`` into ``cgr_mpnn_3D/_amd/lib/``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_float, c_int32, c_int64, c_uint64, c_void_p
+
+_LIB_NAME = "libcgr_mpnn3d.so"
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("CGR_MPNN3D_LIB", os.path.join(_HERE, "lib", _LIB_NAME))
+
+ABI_VERSION = 1
+MAX_DEPTH = 32
+ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
+
+
+class CgrGnnConfig(ctypes.Structure):
+    _fields_ = [
+        ("num_node_features", c_int32),
+        ("num_edge_features", c_int32),
+        ("hidden", c_int32),
+        ("depth", c_int32),
+        ("activation", c_int32),
+        ("learnable_skip", c_int32),
+    ]
+
+
+class CgrBatch(ctypes.Structure):
+    _fields_ = [
+        ("x", c_void_p),
+        ("edge_index", c_void_p),
+        ("edge_attr", c_void_p),
+        ("batch", c_void_p),
+        ("graph_ptr", c_void_p),
+        ("num_nodes", c_int64),
+        ("num_edges", c_int64),
+        ("num_graphs", c_int64),
+    ]
+
+
+# (name, restype, argtypes) of every symbol in include/cgr_mpnn3d.h
+SIGNATURES = [
+    ("cgr_abi_version", c_int32, []),
+    ("cgr_last_error", c_char_p, []),
+    ("cgr_gnn_num_params", c_int32, [POINTER(CgrGnnConfig)]),
+    ("cgr_gnn_arena_bytes", c_int64, [POINTER(CgrGnnConfig), c_int64, c_int64, c_int64]),
+    ("cgr_gnn_workspace_bytes", c_int64, [POINTER(CgrGnnConfig), c_int64, c_int64, c_int64]),
+    ("cgr_gnn_arena_offset", c_int64,
+     [POINTER(CgrGnnConfig), c_int64, c_int64, c_int64, c_char_p, c_int32]),
+    ("cgr_graph_prep", c_int32, [POINTER(CgrGnnConfig), POINTER(CgrBatch), c_void_p, c_void_p]),
+    ("cgr_gnn_forward", c_int32,
+     [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
+      c_int32, c_void_p, c_void_p, c_void_p]),
+    ("cgr_gnn_backward", c_int32,
+     [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
+      c_int32, c_void_p, c_void_p, POINTER(c_void_p), c_void_p, c_void_p]),
+    ("cgr_segment_sum", c_int32,
+     [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
+    ("cgr_dmpnn_conv_scratch_bytes", c_int64, [c_int64, c_int64, c_int64]),
+    ("cgr_dmpnn_conv_forward", c_int32,
+     [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+      c_void_p, c_void_p]),
+    ("cgr_dmpnn_conv_backward", c_int32,
+     [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+      c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("cgr_profile_enable", c_int32, [c_int32]),
+    ("cgr_profile_collect", c_int32, []),
+    ("cgr_profile_reset", None, []),
+    ("cgr_profile_report", c_int64, [c_char_p, c_int64]),
+]
+
+_lib = None
+_load_error: Exception | None = None
+
+
+def load(path: str | None = None):
+    """Load (once) and return the ctypes library; raise RuntimeError if it is unavailable."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    try:
+        lib = ctypes.CDLL(p, mode=ctypes.RTLD_LOCAL)
+    except OSError as e:  # no silent fallback: the product path needs the HIP library
+        _load_error = e
+        raise RuntimeError(
+            f"cgr_mpnn_3D: native HIP library not loadable ({p}): {e}. Build it with "
+            f"`python -c 'import __graft_entry__ as g; g.build()'` or "
+            f"`make -C cgr-mpnn-3d_amd/csrc`.") from e
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.cgr_abi_version()
+    if v != ABI_VERSION:
+        raise RuntimeError(f"cgr_mpnn_3D: ABI version mismatch (lib {v}, python {ABI_VERSION})")
+    _lib = lib
+    return lib
+
+
+def check(rc: int):
+    if rc != 0:
+        msg = load().cgr_last_error()
+        raise RuntimeError(msg.decode() if msg else f"cgr_mpnn_3D native call failed ({rc})")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr(device) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def profile_report() -> dict:
+    """{kernel class: (launches, total_ms)} accumulated since the last cgr_profile_reset()."""
+    lib = load()
+    check(lib.cgr_profile_collect())
+    n = lib.cgr_profile_report(None, 0)
+    buf = ctypes.create_string_buffer(int(n))
+    lib.cgr_profile_report(buf, n)
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, cnt, ms = line.split()
+        out[name] = (int(cnt), float(ms))
+    return out

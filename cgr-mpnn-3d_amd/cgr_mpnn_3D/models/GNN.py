@@ -1,0 +1,199 @@
+"""Drop-in ``cgr_mpnn_3D.models.GNN`` for MI355X.
+
+Same module path, class names, constructor arguments, attribute names and ``state_dict`` keys as
+the reference (``cgr_mpnn_3D/models/GNN.py:8-145`` of tobjec/CGR-MPNN-3D), so ``train.py``,
+``test.py`` and ``hyperparameter_tuning.py`` run unchanged, and the random initialisation for a
+given ``torch.manual_seed`` is identical (parameters are created in the reference's order).
+
+What differs is underneath: ``GNN.forward`` is one call into ``libcgr_mpnn3d.so`` (HIP kernels for
+gfx950) through ``cgr_mpnn_3D._amd.functional.GNNFunction``; the backward is one more call.  There
+is no CPU/PyTorch fallback: CPU tensors or a missing library raise.  ``torch_geometric`` is not
+required; PyG ``Batch``/``Data`` objects are accepted by duck typing (``x``, ``edge_index``,
+``edge_attr``, ``batch`` and optionally ``ptr`` / ``num_graphs``).
+
+Reference behaviours kept on purpose:
+* ``hidden_sizes`` / ``dropout_ps`` shorter than ``depth`` raise ``IndexError`` in ``__init__``
+  (``GNN.py:59-60``) / ``forward`` (``GNN.py:100-102``);
+* non-uniform hidden sizes are rejected at ``forward`` (the reference fails there on shapes);
+* ``batch=None`` pools the whole graph (``global_add_pool(h, None)``), output shape ``[1]``;
+* dropout only in training mode (``F.dropout(..., training=self.training)``).
+Deliberate deviations: the readout's discarded ``lin`` output (``GNN.py:105``) is not
+computed; the scatter size is ``num_nodes`` instead of ``max(dst)+1`` (identical whenever the
+batch's last node has an incoming edge; ``CGR_STRICT=1`` raises like the reference otherwise);
+dropout masks come from a counter-based RNG seeded from torch's CPU generator, not ATen's.
+"""
+
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .._amd import config as _config
+from .._amd import native
+from .._amd.functional import gnn_forward
+from .._amd.pool import global_add_pool, is_add_pool
+
+__all__ = ["GNN", "DMPNNConv", "global_add_pool"]
+
+
+def _activation_code(fn) -> int:
+    if fn is F.relu or fn is torch.relu:
+        return native.ACT_RELU
+    if fn is F.silu:
+        return native.ACT_SILU
+    if fn is F.gelu:
+        return native.ACT_GELU
+    name = getattr(fn, "__name__", "")
+    table = {"relu": native.ACT_RELU, "silu": native.ACT_SILU, "gelu": native.ACT_GELU}
+    if name in table:
+        return table[name]
+    raise NotImplementedError(
+        f"cgr_mpnn_3D (MI355X): activation_fn {fn!r} has no native kernel; supported are "
+        "F.relu, F.silu, F.gelu (train.py:284-292)")
+
+
+class GNN(nn.Module):
+    """Directed message-passing network over condensed reaction graphs (GNN.py:8-110)."""
+
+    def __init__(
+        self,
+        num_node_features: int,
+        num_edge_features: int,
+        depth: int = 3,
+        hidden_sizes: list = None,
+        dropout_ps: list = None,
+        activation_fn=F.relu,
+        aggr: str = "add",
+        pooling_fn=global_add_pool,
+        use_learnable_skip: bool = False,
+    ):
+        super().__init__()
+        self.depth = depth
+        self.hidden_sizes = hidden_sizes or [300] * depth
+        self.dropout_ps = dropout_ps or [0.02] * depth
+        self.activation_fn = activation_fn
+        self.pooling_fn = pooling_fn
+        self.use_learnable_skip = use_learnable_skip
+
+        # parameter creation order == reference order (same init under torch.manual_seed)
+        width0 = self.hidden_sizes[0]
+        self.edge_init = nn.Linear(num_node_features + num_edge_features, width0)
+        self.convs = nn.ModuleList(
+            DMPNNConv(self.hidden_sizes[i], aggr=aggr) for i in range(self.depth))
+        width = self.hidden_sizes[-1]
+        self.edge_to_node = nn.Linear(num_node_features + width, width)
+        self.ffn = nn.Linear(width, 1)
+        if self.use_learnable_skip:
+            self.skip_weights = nn.ParameterList(
+                nn.Parameter(torch.tensor(1.0)) for _ in range(self.depth))
+        # gradient-bucket hook (RCCL all-reduce), set by cgr_mpnn_3D._amd.ddp
+        self._grad_bucket_hook = None
+
+    # -- helpers -------------------------------------------------------------------------------
+    def native_parameters(self):
+        """Parameters in the C-ABI table order (== reference state_dict order)."""
+        ps = [self.edge_init.weight, self.edge_init.bias]
+        for conv in self.convs:
+            ps += [conv.lin.weight, conv.lin.bias]
+        ps += [self.edge_to_node.weight, self.edge_to_node.bias, self.ffn.weight, self.ffn.bias]
+        if self.use_learnable_skip:
+            ps += list(self.skip_weights)
+        return ps
+
+    def _uniform_hidden(self) -> int:
+        widths = {self.edge_init.out_features, self.edge_to_node.out_features}
+        widths |= {conv.lin.out_features for conv in self.convs}
+        if len(widths) != 1:
+            raise RuntimeError(
+                f"GNN: hidden sizes {sorted(widths)} differ; the D-MPNN skip connection "
+                "(GNN.py:94-97) needs one uniform hidden size")
+        return widths.pop()
+
+    # -- forward -------------------------------------------------------------------------------
+    def forward(self, data):
+        x, edge_index, edge_attr, batch = data.x, data.edge_index, data.edge_attr, data.batch
+        if not x.is_cuda:
+            raise RuntimeError(
+                "cgr_mpnn_3D (MI355X) runs on the GPU only: move the model and the batch to "
+                "'cuda' (there is no CPU fallback)")
+        if not is_add_pool(self.pooling_fn):
+            raise NotImplementedError(
+                "cgr_mpnn_3D (MI355X): only global_add_pool is fused into the native head")
+        for conv in self.convs:
+            if conv.aggr != "add":
+                raise NotImplementedError(
+                    f"cgr_mpnn_3D (MI355X): aggr={conv.aggr!r}; the native D-MPNN implements "
+                    "aggr='add' (the reference default)")
+        act = _activation_code(self.activation_fn)
+        H = self._uniform_hidden()
+        drop = [float(self.dropout_ps[l]) for l in range(self.depth)]  # IndexError like GNN.py:101
+
+        dev = x.device
+        x = x.to(dtype=torch.float32).contiguous()
+        edge_index = edge_index.to(device=dev, dtype=torch.int64).contiguous()
+        F_ = x.shape[1]
+        Fe = self.edge_init.in_features - F_
+        if edge_attr is None:
+            edge_attr = x.new_zeros((edge_index.shape[1], 0))
+        edge_attr = edge_attr.to(device=dev, dtype=torch.float32).contiguous()
+        if edge_attr.dim() != 2 or edge_attr.shape[1] != Fe:
+            raise RuntimeError(
+                f"GNN: edge_init expects {self.edge_init.in_features} = num_node_features + "
+                f"num_edge_features inputs, got x[:, {F_}] and edge_attr {tuple(edge_attr.shape)}")
+        if self.edge_to_node.in_features != F_ + H:
+            raise RuntimeError("GNN: edge_to_node input width does not match x")
+        if edge_index.shape[1] % 2:
+            raise RuntimeError("GNN: edge_index must hold reverse-edge pairs (GNN.py:136-138)")
+
+        graph_ptr = None
+        if batch is None:
+            num_graphs = 1
+        else:
+            batch = batch.to(device=dev, dtype=torch.int64).contiguous()
+            ptr = getattr(data, "ptr", None)
+            if ptr is not None and ptr.numel() >= 2 and ptr.is_cuda:
+                graph_ptr = ptr.to(dtype=torch.int64).contiguous()
+                num_graphs = graph_ptr.numel() - 1
+            else:
+                ng = getattr(data, "num_graphs", None)
+                num_graphs = int(ng) if ng is not None else int(batch.max()) + 1
+        if _config.strict and int(edge_index[1].max()) + 1 != x.shape[0]:
+            # the reference's cat([x, s]) (GNN.py:106) fails when the last node has no in-edge
+            raise RuntimeError(
+                "Sizes of tensors must match: scatter size max(edge_index[1])+1 != num_nodes")
+
+        params = self.native_parameters()
+        for p in params:
+            if p.dtype != torch.float32 or not p.is_cuda:
+                raise RuntimeError("cgr_mpnn_3D (MI355X): parameters must be fp32 CUDA tensors")
+        training = self.training and any(p > 0 for p in drop)
+        seed = int(torch.randint(0, 2**62, (1,)).item()) if training else 0
+        return gnn_forward((F_, Fe, H, self.depth, act, self.use_learnable_skip), x, edge_index,
+                           edge_attr, batch, graph_ptr, num_graphs, drop, seed, training,
+                           [p.contiguous() for p in params], self._grad_bucket_hook)
+
+
+class DMPNNConv(nn.Module):
+    """One directed message-passing step (GNN.py:113-145).
+
+    ``forward(edge_index, edge_attr) -> (a, h')`` with ``a[v] = sum_{dst(e)=v} edge_attr[e]`` and
+    ``h'[e] = lin(a[src(e)] - edge_attr[e ^ 1])``.  Runs on the native segmented-sum + gathered
+    MFMA GEMM kernels (``cgr_dmpnn_conv_forward``/``_backward``).  ``GNN.forward`` does not call
+    it: the fused path inlines it.
+    """
+
+    def __init__(self, hidden_size: int, aggr="add"):
+        super().__init__()
+        self.aggr = aggr
+        self.lin = nn.Linear(hidden_size, hidden_size)
+
+    def forward(self, edge_index, edge_attr):
+        from .._amd.conv import dmpnn_conv
+
+        if self.aggr != "add":
+            raise NotImplementedError("DMPNNConv (MI355X): only aggr='add' is native")
+        return dmpnn_conv(edge_index, edge_attr, self.lin.weight, self.lin.bias)
+
+    def message(self, edge_attr):
+        return edge_attr

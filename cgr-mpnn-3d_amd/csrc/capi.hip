@@ -1,0 +1,314 @@
+// C ABI of libcgr_mpnn3d.so (include/cgr_mpnn3d.h): validation, arena/workspace layout, error
+// reporting.  No entry point allocates or synchronises; all work is enqueued on `stream`.
+#include <string.h>
+
+#include <string>
+
+#include "dispatch.hpp"
+#include "gnn_internal.hpp"
+#include "kernels.hpp"
+
+namespace cgr {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
+                     const float* dropout_p, uint64_t seed, int training, void* arena, float* y,
+                     hipStream_t st);
+int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
+                      const float* dropout_p, uint64_t seed, int training, const void* arena,
+                      const float* dy, float* const* grads, void* workspace, hipStream_t st);
+
+Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
+  Dims d;
+  d.N = N;
+  d.E = E;
+  d.B = B;
+  d.F = cfg->num_node_features;
+  d.Fe = cfg->num_edge_features;
+  d.Fep = (int)round_up(d.Fe, 4);
+  d.H = cfg->hidden;
+  d.Hp = (int)round_up(d.H, 4);
+  d.D = cfg->depth;
+  d.act = cfg->activation;
+  d.learnable_skip = cfg->learnable_skip ? 1 : 0;
+  return d;
+}
+
+namespace {
+struct Bump {
+  size_t off = 0;
+  size_t take(size_t bytes) {
+    const size_t o = off;
+    off = (size_t)round_up((int64_t)(off + bytes), (int64_t)kAlign);
+    return o;
+  }
+};
+constexpr size_t kNone = (size_t)-1;
+}  // namespace
+
+ArenaLayout arena_layout(const Dims& d) {
+  ArenaLayout L;
+  memset(&L, 0xff, sizeof(L));
+  Bump b;
+  const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
+  // zero block: six int arrays back to back, padded to a multiple of 16 bytes
+  L.zero_block = b.off;
+  L.deg_dst = b.off;
+  L.deg_src = L.deg_dst + 4 * N;
+  L.cursor = L.deg_src + 4 * N;
+  L.cursor2 = L.cursor + 4 * N;
+  L.graph_cnt = L.cursor2 + 4 * N;
+  L.status = L.graph_cnt + 4 * B;
+  L.zero_bytes = (size_t)round_up((int64_t)(4 * (4 * N + B) + 16), 16);
+  b.take(L.zero_bytes);
+  L.perm = b.take(4 * E);
+  L.src_s = b.take(4 * E);
+  L.dst_s = b.take(4 * E);
+  L.rev_s = b.take(4 * E);
+  L.src_list = b.take(4 * E);
+  L.inv = b.take(4 * E);
+  L.src_c = b.take(4 * E);
+  L.dst_c = b.take(4 * E);
+  L.dst_ptr = b.take(4 * (N + 1));
+  L.src_ptr = b.take(4 * (N + 1));
+  L.graph_ptr = b.take(4 * (B + 1));
+  L.node_graph = b.take(4 * N);
+  L.e_s = d.Fep ? b.take(4 * E * (size_t)d.Fep) : kNone;
+  L.w0eT = d.Fe ? b.take(4 * (size_t)d.Fe * Hp) : kNone;
+  L.P = b.take(4 * N * Hp);
+  for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
+    L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
+    L.a[l] = l <= d.D ? b.take(4 * N * Hp) : kNone;
+    L.pre[l] = (l <= d.D && d.act != CGR_ACT_RELU) ? b.take(4 * E * Hp) : kNone;
+  }
+  L.zn = d.act != CGR_ACT_RELU ? b.take(4 * N * Hp) : kNone;
+  L.hn = b.take(4 * N * Hp);
+  L.g = b.take(4 * B * Hp);
+  L.bytes = b.off;
+  L.off_index_begin = 0;
+  return L;
+}
+
+static inline void* at(void* base, size_t off) {
+  return off == kNone ? nullptr : static_cast<char*>(base) + off;
+}
+
+IndexView index_view(void* arena, const ArenaLayout& L) {
+  IndexView v;
+  v.deg_dst = (int*)at(arena, L.deg_dst);
+  v.deg_src = (int*)at(arena, L.deg_src);
+  v.cursor = (int*)at(arena, L.cursor);
+  v.cursor2 = (int*)at(arena, L.cursor2);
+  v.graph_cnt = (int*)at(arena, L.graph_cnt);
+  v.status = (int*)at(arena, L.status);
+  v.zero_block = at(arena, L.zero_block);
+  v.zero_bytes = L.zero_bytes;
+  v.perm = (int*)at(arena, L.perm);
+  v.src_s = (int*)at(arena, L.src_s);
+  v.dst_s = (int*)at(arena, L.dst_s);
+  v.rev_s = (int*)at(arena, L.rev_s);
+  v.src_list = (int*)at(arena, L.src_list);
+  v.inv = (int*)at(arena, L.inv);
+  v.src_c = (int*)at(arena, L.src_c);
+  v.dst_c = (int*)at(arena, L.dst_c);
+  v.dst_ptr = (int*)at(arena, L.dst_ptr);
+  v.src_ptr = (int*)at(arena, L.src_ptr);
+  v.graph_ptr = (int*)at(arena, L.graph_ptr);
+  v.node_graph = (int*)at(arena, L.node_graph);
+  return v;
+}
+
+FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
+  FloatView f;
+  f.e_s = (float*)at(arena, L.e_s);
+  f.w0eT = (float*)at(arena, L.w0eT);
+  f.P = (float*)at(arena, L.P);
+  for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
+    f.h[l] = (float*)at(arena, L.h[l]);
+    f.a[l] = (float*)at(arena, L.a[l]);
+    f.pre[l] = (float*)at(arena, L.pre[l]);
+  }
+  f.zn = (float*)at(arena, L.zn);
+  f.hn = (float*)at(arena, L.hn);
+  f.g = (float*)at(arena, L.g);
+  (void)d;
+  return f;
+}
+
+WorkspaceLayout workspace_layout(const Dims& d) {
+  WorkspaceLayout W;
+  Bump b;
+  const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
+  W.dpre = b.take(4 * E * Hp);
+  W.dm = b.take(4 * E * Hp);
+  W.dh0 = b.take(4 * E * Hp);
+  W.da = b.take(4 * N * Hp);
+  W.dzn = b.take(4 * N * Hp);
+  W.ds = b.take(4 * N * Hp);
+  W.Gs = b.take(4 * N * Hp);
+  W.dg = b.take(4 * B * Hp);
+  W.wT = b.take(4 * (size_t)(d.D + 1) * d.H * Hp);
+  size_t slab = 0, bslab = 0;
+  auto acc = [&](int Nout, int Kout, int64_t R) {
+    const TnPlan p = tn_plan(Nout, Kout, (int)R);
+    const size_t s = (size_t)p.splits * Nout * Kout, bs = (size_t)p.splits * Nout;
+    slab = s > slab ? s : slab;
+    bslab = bs > bslab ? bs : bslab;
+  };
+  acc(d.H, d.F + d.H, d.N);
+  acc(d.H, d.H, d.E);
+  if (d.Fe > 0) acc(d.H, d.Fe, d.E);
+  if (d.F > 0) acc(d.H, d.F, d.N);
+  W.slab_elems = slab;
+  W.bslab_elems = bslab;
+  W.slab = b.take(4 * slab);
+  W.bslab = b.take(4 * bslab);
+  W.dsig_blocks = layer_act_bwd_blocks(d.E, d.Hp);
+  W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
+  W.bytes = b.off;
+  return W;
+}
+
+static int validate_config(const cgr_gnn_config* c) {
+  CGR_CHECK(c != nullptr, "cgr: config is NULL");
+  CGR_CHECK(c->num_node_features >= 0, "cgr: num_node_features must be >= 0");
+  CGR_CHECK(c->num_edge_features >= 0, "cgr: num_edge_features must be >= 0");
+  CGR_CHECK(c->hidden >= 1, "cgr: hidden size must be >= 1");
+  CGR_CHECK(c->depth >= 1 && c->depth <= CGR_MAX_DEPTH, "cgr: depth must be in [1, 32]");
+  CGR_CHECK(c->activation >= 0 && c->activation <= 2, "cgr: unknown activation code");
+  return 0;
+}
+
+static int validate_batch(const cgr_gnn_config* c, const cgr_batch* b) {
+  CGR_CHECK(b != nullptr, "cgr: batch is NULL");
+  CGR_CHECK(b->num_nodes >= 1 && b->num_nodes < (1ll << 31), "cgr: num_nodes out of range");
+  CGR_CHECK(b->num_edges >= 1 && b->num_edges < (1ll << 30),
+            "cgr: num_edges must be >= 1 (the reference's flip/view needs edge pairs)");
+  CGR_CHECK(b->num_edges % 2 == 0,
+            "cgr: num_edges must be even: reverse edge of e is e^1 (GNN.py:136-138)");
+  CGR_CHECK(b->num_graphs >= 1 && b->num_graphs <= b->num_nodes, "cgr: num_graphs out of range");
+  CGR_CHECK(b->batch != nullptr || b->graph_ptr != nullptr || b->num_graphs == 1,
+            "cgr: batch == NULL requires num_graphs == 1");
+  CGR_CHECK(b->edge_index != nullptr, "cgr: edge_index is NULL");
+  CGR_CHECK(c->num_node_features == 0 || b->x != nullptr, "cgr: x is NULL");
+  CGR_CHECK(c->num_edge_features == 0 || b->edge_attr != nullptr, "cgr: edge_attr is NULL");
+  return 0;
+}
+
+}  // namespace cgr
+
+using namespace cgr;
+
+extern "C" {
+
+int cgr_abi_version(void) { return CGR_ABI_VERSION; }
+
+const char* cgr_last_error(void) { return g_err.c_str(); }
+
+int cgr_gnn_num_params(const cgr_gnn_config* cfg) {
+  if (validate_config(cfg)) return -1;
+  return 6 + 2 * cfg->depth + (cfg->learnable_skip ? cfg->depth : 0);
+}
+
+int64_t cgr_gnn_arena_bytes(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
+  if (validate_config(cfg)) return -1;
+  return (int64_t)arena_layout(make_dims(cfg, N, E, B)).bytes;
+}
+
+int64_t cgr_gnn_workspace_bytes(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
+  if (validate_config(cfg)) return -1;
+  return (int64_t)workspace_layout(make_dims(cfg, N, E, B)).bytes;
+}
+
+int64_t cgr_gnn_arena_offset(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B,
+                             const char* name, int32_t index) {
+  if (validate_config(cfg) || name == nullptr) return -1;
+  const ArenaLayout L = arena_layout(make_dims(cfg, N, E, B));
+  size_t o = (size_t)-1;
+  const std::string n(name);
+  const bool li = index >= 0 && index <= CGR_MAX_DEPTH;
+  if (n == "status") o = L.status;
+  else if (n == "perm") o = L.perm;
+  else if (n == "src_s") o = L.src_s;
+  else if (n == "dst_s") o = L.dst_s;
+  else if (n == "rev_s") o = L.rev_s;
+  else if (n == "src_list") o = L.src_list;
+  else if (n == "dst_ptr") o = L.dst_ptr;
+  else if (n == "src_ptr") o = L.src_ptr;
+  else if (n == "graph_ptr") o = L.graph_ptr;
+  else if (n == "node_graph") o = L.node_graph;
+  else if (n == "e_s") o = L.e_s;
+  else if (n == "P") o = L.P;
+  else if (n == "h" && li) o = L.h[index];
+  else if (n == "a" && li) o = L.a[index];
+  else if (n == "pre" && li) o = L.pre[index];
+  else if (n == "zn") o = L.zn;
+  else if (n == "hn") o = L.hn;
+  else if (n == "g") o = L.g;
+  return o == (size_t)-1 ? -1 : (int64_t)o;
+}
+
+int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* b, void* arena, void* stream) {
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  rc = validate_batch(cfg, b);
+  if (rc) return rc;
+  CGR_CHECK(arena != nullptr, "cgr: arena is NULL");
+  const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
+  const ArenaLayout L = arena_layout(d);
+  const FloatView fv = float_view(arena, L, d);
+  PrepArgs pa{b->edge_index, b->batch, b->graph_ptr, b->edge_attr, d.N, d.E, d.B,
+              d.Fe,          d.Fep,   index_view(arena, L), fv.e_s};
+  return cgr_graph_prep_impl(pa, (hipStream_t)stream);
+}
+
+int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,
+                    const float* dropout_p, uint64_t seed, int32_t training, void* arena, float* y,
+                    void* stream) {
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  rc = validate_batch(cfg, b);
+  if (rc) return rc;
+  CGR_CHECK(params != nullptr && arena != nullptr && y != nullptr,
+            "cgr: params / arena / y must not be NULL");
+  const int np = cgr_gnn_num_params(cfg);
+  for (int i = 0; i < np; ++i) CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
+  const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
+  return gnn_forward_impl(d, params, b, dropout_p, seed, training, arena, y, (hipStream_t)stream);
+}
+
+int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,
+                     const float* dropout_p, uint64_t seed, int32_t training, const void* arena,
+                     const float* dy, float* const* grads, void* workspace, void* stream) {
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  rc = validate_batch(cfg, b);
+  if (rc) return rc;
+  CGR_CHECK(params != nullptr && arena != nullptr && dy != nullptr && grads != nullptr &&
+                workspace != nullptr,
+            "cgr: params / arena / dy / grads / workspace must not be NULL");
+  const int np = cgr_gnn_num_params(cfg);
+  for (int i = 0; i < np; ++i) {
+    CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
+    CGR_CHECK(grads[i] != nullptr, "cgr: NULL gradient pointer");
+  }
+  const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
+  return gnn_backward_impl(d, params, b, dropout_p, seed, training, arena, dy, grads, workspace,
+                           (hipStream_t)stream);
+}
+
+int cgr_segment_sum(const float* values, int64_t ld_values, const int32_t* index,
+                    const int32_t* seg_ptr, int64_t num_segments, int64_t width, float* out,
+                    int64_t ld_out, void* stream) {
+  CGR_CHECK(values != nullptr && seg_ptr != nullptr && out != nullptr,
+            "cgr_segment_sum: NULL pointer");
+  CGR_CHECK(num_segments >= 0 && width >= 0 && ld_values >= width && ld_out >= width,
+            "cgr_segment_sum: bad sizes");
+  HIP_RET(segment_sum(values, ld_values, index, seg_ptr, num_segments, width, out, ld_out,
+                      (hipStream_t)stream));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,127 @@
+// Shared device helpers for the CGR-MPNN-3D HIP kernels (gfx950 / CDNA4 only).
+//
+// Conventions (DESIGN.md "Data layout in HBM"):
+//   * every per-edge activation is an [E, Hp] fp32 row-major matrix in *dst-sorted* edge order
+//     (position i, see graph_prep.hip); every per-node activation is [N, Hp]; Hp = round_up(H, 4)
+//     so rows are 16-byte aligned and all internal loads are float4;
+//   * external tensors (x, edge_attr, weights) keep the caller's layout; loaders read them with a
+//     vector width VEC in {4, 2, 1} chosen on the host from the leading dimension and alignment.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cgr {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+enum Act : int { ACT_RELU = 0, ACT_SILU = 1, ACT_GELU = 2 };
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? z : 0.f;
+  if (act == ACT_SILU) return z / (1.f + __expf(-z));
+  // GELU, exact erf form (F.gelu default approximate='none')
+  return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+}
+
+// d act / dz.  ReLU: 0 at z == 0 (ATen threshold_backward).
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_SILU) {
+    const float s = 1.f / (1.f + __expf(-z));
+    return s * (1.f + z * (1.f - s));
+  }
+  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+  const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
+  return cdf + z * pdf;
+}
+
+// Counter-based dropout RNG: keep(seed, layer, element) is a pure function, so the backward
+// regenerates the mask instead of storing it.  splitmix64 finaliser over a 64-bit counter.
+__device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint32_t layer, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1) + (uint64_t(layer) << 56);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return uint32_t(z >> 32);
+}
+
+// keep with probability 1-p: hash >= p * 2^32
+__device__ __forceinline__ bool drop_keep(uint64_t seed, uint32_t layer, uint64_t idx,
+                                          uint32_t thresh) {
+  return drop_hash(seed, layer, idx) >= thresh;
+}
+
+__device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+
+__device__ __forceinline__ float4 f4sub(float4 a, float4 b) {
+  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+__device__ __forceinline__ float4 f4add(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// Load 4 consecutive floats p[0..3] of a row whose valid length from p is `valid` (elements at
+// index >= valid read as 0).  VEC = guaranteed alignment/divisibility of the row and of the
+// logical length: sub-chunks of VEC are either fully valid or fully invalid.
+template <int VEC>
+__device__ __forceinline__ float4 load4(const float* __restrict__ p, int valid) {
+  if constexpr (VEC == 4) {
+    if (valid <= 0) return f4zero();
+    float4 v = *reinterpret_cast<const float4*>(p);
+    if (valid < 4) {  // only internal [*, Hp] rows (Hp = round_up(H, 4)) reach this
+      if (valid < 2) v.y = 0.f;
+      if (valid < 3) v.z = 0.f;
+      v.w = 0.f;
+    }
+    return v;
+  } else if constexpr (VEC == 2) {
+    float4 r = f4zero();
+    if (valid > 0) {
+      const float2 u = *reinterpret_cast<const float2*>(p);
+      r.x = u.x;
+      r.y = valid > 1 ? u.y : 0.f;
+    }
+    if (valid > 2) {
+      const float2 u = *reinterpret_cast<const float2*>(p + 2);
+      r.z = u.x;
+      r.w = valid > 3 ? u.y : 0.f;
+    }
+    return r;
+  } else {
+    float4 r;
+    r.x = valid > 0 ? p[0] : 0.f;
+    r.y = valid > 1 ? p[1] : 0.f;
+    r.z = valid > 2 ? p[2] : 0.f;
+    r.w = valid > 3 ? p[3] : 0.f;
+    return r;
+  }
+}
+
+// internal [*, Hp] buffers: chunk is always in-bounds of the padded row; zero beyond `valid`
+__device__ __forceinline__ float4 load4_masked_internal(const float* __restrict__ p, int valid) {
+  if (valid <= 0) return f4zero();
+  float4 v = *reinterpret_cast<const float4*>(p);
+  if (valid < 4) {
+    if (valid < 2) v.y = 0.f;
+    if (valid < 3) v.z = 0.f;
+    v.w = 0.f;
+  }
+  return v;
+}
+
+__device__ __forceinline__ float f4get(const float4& v, int i) {
+  return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
+}
+
+__host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+__host__ __device__ inline int64_t cdiv(int64_t x, int64_t m) { return (x + m - 1) / m; }
+
+// Wave-level sum (64 lanes).
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace cgr

@@ -1,0 +1,60 @@
+// Host-side tile / vector-width selection shared by forward, backward and workspace sizing.
+#pragma once
+
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "gemm.hpp"
+
+namespace cgr {
+
+template <int V>
+using IC = std::integral_constant<int, V>;
+
+// largest of {4, 2, 1} dividing the leading dimension and the logical row length, with a
+// matching pointer alignment
+inline int vec_for(const void* p, int64_t ld, int64_t K) {
+  const uintptr_t a = (uintptr_t)p;
+  if (ld % 4 == 0 && K % 4 == 0 && a % 16 == 0) return 4;
+  if (ld % 2 == 0 && K % 2 == 0 && a % 8 == 0) return 2;
+  return 1;
+}
+
+template <class F>
+inline auto with_vec(int v, F&& f) {
+  if (v == 4) return f(IC<4>{});
+  if (v == 2) return f(IC<2>{});
+  return f(IC<1>{});
+}
+
+// NT GEMM: 4 waves (BM = 64 rows), RN column fragments: 5 when the output width tiles by 80
+// (H = 400 -> 5 tiles, no waste), else 4 (BN = 64).
+template <class F>
+inline auto with_nt_rn(int N, F&& f) {
+  if (N % 80 == 0) return f(IC<5>{});
+  return f(IC<4>{});
+}
+
+// TN GEMM: WAVES from the output-row count (= H), RN from the output-column count.
+template <class F>
+inline auto with_tn_shape(int Nout, int Kout, F&& f) {
+  if (Nout % 80 == 0) {
+    if (Kout <= 16) return f(IC<5>{}, IC<1>{});
+    if (Kout % 80 == 0) return f(IC<5>{}, IC<5>{});
+    return f(IC<5>{}, IC<4>{});
+  }
+  if (Kout <= 16) return f(IC<4>{}, IC<1>{});
+  if (Kout % 80 == 0) return f(IC<4>{}, IC<5>{});
+  return f(IC<4>{}, IC<4>{});
+}
+
+constexpr int kTnTargetWorkgroups = 1024;  // ~4 per CU on 256 CUs
+
+inline TnPlan tn_plan(int Nout, int Kout, int R) {
+  return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
+    return plan_tn<decltype(W)::value, decltype(RN)::value>(Nout, Kout, R, kTnTargetWorkgroups);
+  });
+}
+
+}  // namespace cgr

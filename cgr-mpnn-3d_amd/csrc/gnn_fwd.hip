@@ -1,0 +1,148 @@
+// GNN.forward (GNN.py:76-110) as a sequence of HIP launches on one stream.
+//
+//   prep          graph bookkeeping (graph_prep.hip)
+//   P   = x W0x^T node-level half of edge init: N*F*H instead of E*F*H FLOPs (no [E, F+Fe] cat)
+//   h0  = act(P[src] + e W0e^T + b0)                                      (GNN.py:85-87)
+//   a0  = segsum_dst(h0)                                                  (GNN.py:134)
+//   for l: h_{l+1} = drop(act((a_l[src] - h_l[rev]) W_l^T + b_l + s_l h0))  gather->MFMA->epilogue
+//          a_{l+1} = segsum_dst(h_{l+1})                                  (GNN.py:90-102, 134)
+//   hn  = act([x | a_D] W_n^T + b_n)   (a_D IS the readout aggregate s)   (GNN.py:105-107)
+//   y   = (sum_{v in graph} hn[v]) . wf + bf                               (GNN.py:110)
+// The reference's discarded readout GEMM (GNN.py:105 -> lin(...) at :141) is not executed.
+#include "dispatch.hpp"
+#include "epilogues.hpp"
+#include "gnn_internal.hpp"
+#include "kernels.hpp"
+#include "profiling.hpp"
+
+namespace cgr {
+
+static void dropout_consts(const float* dropout_p, int training, int l, uint32_t* thresh,
+                           float* scale) {
+  *thresh = 0;
+  *scale = 1.f;
+  if (!training || dropout_p == nullptr) return;
+  const double p = dropout_p[l];
+  if (p <= 0.0) return;
+  if (p >= 1.0) {
+    *thresh = 0xFFFFFFFFu;
+    *scale = 0.f;
+    return;
+  }
+  double t = p * 4294967296.0;
+  if (t > 4294967295.0) t = 4294967295.0;
+  *thresh = (uint32_t)t;
+  if (*thresh == 0) *thresh = 1;
+  *scale = (float)(1.0 / (1.0 - p));
+}
+
+void dropout_params(const float* dropout_p, int training, int l, uint32_t* thresh, float* scale) {
+  dropout_consts(dropout_p, training, l, thresh, scale);
+}
+
+int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
+                     const float* dropout_p, uint64_t seed, int training, void* arena, float* y,
+                     hipStream_t st) {
+  const ArenaLayout L = arena_layout(d);
+  const IndexView iv = index_view(arena, L);
+  const FloatView fv = float_view(arena, L, d);
+  const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
+  const float* W0 = params[CGR_PARAM_EDGE_INIT_W];
+  const float* b0 = params[CGR_PARAM_EDGE_INIT_B];
+
+  PrepArgs pa{b->edge_index, b->batch, b->graph_ptr, b->edge_attr, d.N, d.E, d.B,
+              d.Fe,          d.Fep,   iv,           fv.e_s};
+  {
+    ProfScope _p("graph_prep", st);
+    int rc = cgr_graph_prep_impl(pa, st);
+    if (rc) return rc;
+  }
+
+  // edge-feature slice of edge_init.weight, transposed to [Fe, Hp]
+  if (Fe > 0) {
+    ProfScope _p("weight_transpose", st);
+    TransposeJobs tj{};
+    tj.job[0] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
+    tj.n = 1;
+    HIP_RET(transpose_batch(tj, st));
+  }
+
+  // P = x @ W0[:, :F]^T   [N, Hp]
+  {
+    ProfScope _p("gemm_nt_node_P", st);
+    const int vx = vec_for(b->x, F, F), vw = vec_for(W0, F + Fe, F);
+    hipError_t e = with_vec(vx, [&](auto VX) {
+      return with_vec(vw, [&](auto VW) {
+        return with_nt_rn(H, [&](auto RN) {
+          LdPlain<decltype(VX)::value> al{b->x, F};
+          LdPlain<decltype(VW)::value> bl{W0, F + Fe};
+          EpStore ep{fv.P, Hp, N, H, nullptr};
+          return launch_gemm_nt<4, decltype(RN)::value>(al, bl, ep, N, H, F, st);
+        });
+      });
+    });
+    HIP_RET(e);
+  }
+  {
+    ProfScope _p("edge_init_fwd", st);
+    HIP_RET(edge_init_fwd(fv.P, iv.src_s, fv.e_s, Fe, d.Fep, fv.w0eT, b0, E, H, Hp, d.act,
+                          fv.h[0], fv.pre[0], st));
+  }
+  {
+    ProfScope _p("segsum_dst_fwd", st);
+    HIP_RET(segment_sum(fv.h[0], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[0], Hp, st));
+  }
+
+  for (int l = 0; l < D; ++l) {
+    const float* Wl = params[CGR_PARAM_CONV_W(l)];
+    const float* bl_ = params[CGR_PARAM_CONV_B(l)];
+    uint32_t thresh;
+    float scale;
+    dropout_consts(dropout_p, training, l, &thresh, &scale);
+    EpLayer ep{bl_,      d.learnable_skip ? params[CGR_PARAM_SKIP(D, l)] : nullptr,
+               fv.h[0],  fv.h[l + 1],
+               fv.pre[l + 1], Hp,
+               E,        H,
+               d.act,    thresh,
+               scale,    seed,
+               l};
+    LdGatherDiff<false> al{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
+    const int vw = vec_for(Wl, H, H);
+    ProfScope _p1("gemm_nt_layer_fwd", st);
+    hipError_t e = with_vec(vw, [&](auto VW) {
+      return with_nt_rn(H, [&](auto RN) {
+        LdPlain<decltype(VW)::value> blw{Wl, H};
+        return launch_gemm_nt<4, decltype(RN)::value>(al, blw, ep, E, H, H, st);
+      });
+    });
+    HIP_RET(e);
+    _p1.end();
+    ProfScope _p2("segsum_dst_fwd", st);
+    HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
+  }
+
+  // readout: hn = act([x | s] W_n^T + b_n), s = a_D
+  {
+    ProfScope _p("gemm_nt_readout_fwd", st);
+    const float* Wn = params[CGR_PARAM_E2N_W(D)];
+    const float* bn = params[CGR_PARAM_E2N_B(D)];
+    const int vx = vec_for(b->x, F, F), vw = vec_for(Wn, F + H, F + H);
+    EpReadout ep{bn, fv.hn, fv.zn, Hp, N, H, d.act};
+    hipError_t e = with_vec(vx, [&](auto VX) {
+      return with_vec(vw, [&](auto VW) {
+        return with_nt_rn(H, [&](auto RN) {
+          LdConcat<decltype(VX)::value> al{b->x, F, fv.a[D], Hp, F};
+          LdPlain<decltype(VW)::value> blw{Wn, F + H};
+          return launch_gemm_nt<4, decltype(RN)::value>(al, blw, ep, N, H, F + H, st);
+        });
+      });
+    });
+    HIP_RET(e);
+  }
+  ProfScope _p("pool_head_fwd", st);
+  HIP_RET(pool_head_fwd(fv.hn, Hp, iv.graph_ptr, d.B, H, params[CGR_PARAM_FFN_W(D)],
+                        params[CGR_PARAM_FFN_B(D)], fv.g, y, st));
+  return 0;
+}
+
+}  // namespace cgr

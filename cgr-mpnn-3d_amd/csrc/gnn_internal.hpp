@@ -1,0 +1,117 @@
+// Internal (non-ABI) declarations: arena layout, index views, launch helpers.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/cgr_mpnn3d.h"
+
+namespace cgr {
+
+void set_error(const std::string& msg);
+
+#define HIP_RET(expr)                                                                         \
+  do {                                                                                        \
+    hipError_t _e = (expr);                                                                   \
+    if (_e != hipSuccess) {                                                                   \
+      ::cgr::set_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + __FILE__ + \
+                       ":" + std::to_string(__LINE__));                                       \
+      return CGR_ERR_HIP;                                                                     \
+    }                                                                                         \
+  } while (0)
+
+#define CGR_CHECK(cond, msg)           \
+  do {                                 \
+    if (!(cond)) {                     \
+      ::cgr::set_error(msg);           \
+      return CGR_ERR_INVALID_ARGUMENT; \
+    }                                  \
+  } while (0)
+
+constexpr size_t kAlign = 256;
+
+// Index bookkeeping inside the arena (all int32).
+struct IndexView {
+  // zero block (memset each call): deg_dst, deg_src, cursor, cursor2, graph_cnt, status
+  int* deg_dst;
+  int* deg_src;
+  int* cursor;
+  int* cursor2;
+  int* graph_cnt;
+  int* status;
+  void* zero_block;
+  size_t zero_bytes;
+  int* perm;
+  int* src_s;
+  int* dst_s;
+  int* rev_s;
+  int* src_list;
+  int* inv;
+  int* src_c;
+  int* dst_c;
+  int* dst_ptr;
+  int* src_ptr;
+  int* graph_ptr;
+  int* node_graph;
+};
+
+// Forward-saved float state inside the arena.
+struct FloatView {
+  float* e_s;   // [E, Fep] sorted, zero padded edge_attr
+  float* w0eT;  // [Fe, Hp] transposed edge-feature slice of edge_init.weight
+  float* P;     // [N, Hp]  x @ W0[:, :F]^T (node-level half of edge init)
+  float* h[CGR_MAX_DEPTH + 1];    // [E, Hp] h_0 .. h_D
+  float* a[CGR_MAX_DEPTH + 1];    // [N, Hp] a_l = scatter_add(h_l, dst); a_D = readout s
+  float* pre[CGR_MAX_DEPTH + 1];  // [E, Hp] pre-activations (non-ReLU only; else nullptr)
+  float* zn;                      // [N, Hp] readout pre-activation (non-ReLU only)
+  float* hn;                      // [N, Hp] readout activation
+  float* g;                       // [B, Hp] pooled graph embeddings
+};
+
+struct Dims {
+  int64_t N, E, B;
+  int F, Fe, Fep, H, Hp, D;
+  int act;
+  int learnable_skip;
+};
+
+struct ArenaLayout {
+  size_t off_index_begin;
+  size_t bytes;
+  // offsets (bytes) for every buffer
+  size_t zero_block, zero_bytes, deg_dst, deg_src, cursor, cursor2, graph_cnt, status;
+  size_t perm, src_s, dst_s, rev_s, src_list, inv, src_c, dst_c, dst_ptr, src_ptr, graph_ptr,
+      node_graph;
+  size_t e_s, w0eT, P, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,
+      g;
+};
+
+struct WorkspaceLayout {
+  size_t bytes;
+  size_t dpre, dm, dh0, da, dzn, ds, Gs, dg, wT, slab, bslab, dsig_part, slab_elems, bslab_elems;
+  int dsig_blocks;
+};
+
+Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B);
+ArenaLayout arena_layout(const Dims& d);
+WorkspaceLayout workspace_layout(const Dims& d);
+IndexView index_view(void* arena, const ArenaLayout& L);
+FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d);
+
+struct PrepArgs {
+  const int64_t* edge_index;
+  const int64_t* batch;      // may be null (one graph)
+  const int64_t* graph_ptr;  // may be null (derive from batch)
+  const float* edge_attr;
+  int64_t N, E, B;
+  int64_t Fe, Fep;
+  IndexView idx;
+  float* e_s;
+};
+
+}  // namespace cgr
+
+int cgr_graph_prep_impl(const cgr::PrepArgs& a, hipStream_t st);

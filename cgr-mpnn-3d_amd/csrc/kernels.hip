@@ -1,0 +1,433 @@
+// Non-GEMM kernels of the D-MPNN path: segmented sums (the sum-scatter of GNN.py:134 / :110),
+// edge init, pooling + ffn head, backward activation kernels, deterministic split-K reduction.
+// All are HBM/L2-streaming kernels: float4 per lane along the hidden dimension, rows of one
+// segment are contiguous (dst-sorted edges) so every wave reads whole 1.6 KB rows.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace cgr {
+
+// ------------------------------------------------------------------------------------------
+// segmented sum
+// ------------------------------------------------------------------------------------------
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_segsum_v4(const float* __restrict__ vals, int64_t ldv,
+                                                   const int* __restrict__ idx,
+                                                   const int* __restrict__ ptr, int64_t nseg,
+                                                   int C4, float* __restrict__ out, int64_t ldo) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nseg * C4) return;
+  const int64_t v = t / C4;
+  const int c = (int)(t - v * C4);
+  const int b = ptr[v], e = ptr[v + 1];
+  float4 acc = f4zero();
+  for (int j = b; j < e; ++j) {
+    const int64_t row = GATHER ? idx[j] : j;
+    acc = f4add(acc, *reinterpret_cast<const float4*>(vals + row * ldv + 4 * c));
+  }
+  *reinterpret_cast<float4*>(out + v * ldo + 4 * c) = acc;
+}
+
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_segsum_s(const float* __restrict__ vals, int64_t ldv,
+                                                  const int* __restrict__ idx,
+                                                  const int* __restrict__ ptr, int64_t nseg,
+                                                  int W, float* __restrict__ out, int64_t ldo) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nseg * W) return;
+  const int64_t v = t / W;
+  const int c = (int)(t - v * W);
+  const int b = ptr[v], e = ptr[v + 1];
+  float acc = 0.f;
+  for (int j = b; j < e; ++j) {
+    const int64_t row = GATHER ? idx[j] : j;
+    acc += vals[row * ldv + c];
+  }
+  out[v * ldo + c] = acc;
+}
+
+hipError_t segment_sum(const float* vals, int64_t ldv, const int* idx, const int* ptr,
+                       int64_t nseg, int64_t width, float* out, int64_t ldo, hipStream_t st) {
+  if (nseg <= 0 || width <= 0) return hipSuccess;
+  const bool v4 = (width % 4 == 0) && (ldv % 4 == 0) && (ldo % 4 == 0) &&
+                  ((uintptr_t)vals % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  const int T = 256;
+  if (v4) {
+    const int C4 = (int)(width / 4);
+    const int64_t tot = nseg * C4;
+    if (idx)
+      hipLaunchKernelGGL(k_segsum_v4<true>, dim3(cdiv(tot, T)), dim3(T), 0, st, vals, ldv, idx,
+                         ptr, nseg, C4, out, ldo);
+    else
+      hipLaunchKernelGGL(k_segsum_v4<false>, dim3(cdiv(tot, T)), dim3(T), 0, st, vals, ldv, idx,
+                         ptr, nseg, C4, out, ldo);
+  } else {
+    const int64_t tot = nseg * width;
+    if (idx)
+      hipLaunchKernelGGL(k_segsum_s<true>, dim3(cdiv(tot, T)), dim3(T), 0, st, vals, ldv, idx,
+                         ptr, nseg, (int)width, out, ldo);
+    else
+      hipLaunchKernelGGL(k_segsum_s<false>, dim3(cdiv(tot, T)), dim3(T), 0, st, vals, ldv, idx,
+                         ptr, nseg, (int)width, out, ldo);
+  }
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// batched 32x32-tiled transpose
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_transpose(TransposeJobs jobs) {
+  const TransposeJob jb = jobs.job[blockIdx.y];
+  const int tr = (jb.rows + 31) / 32, tc = (jb.cols + 31) / 32;
+  const int tile = blockIdx.x;
+  if (tile >= tr * tc) return;
+  const int r0 = (tile / tc) * 32, c0 = (tile % tc) * 32;
+  __shared__ float s[32][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + tx;
+    s[i][tx] = (r < jb.rows && c < jb.cols) ? jb.src[(int64_t)r * jb.ld_src + jb.col_off + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + tx;
+    if (r < jb.rows && c < jb.cols) jb.dst[(int64_t)c * jb.ld_dst + r] = s[tx][i];
+  }
+}
+
+hipError_t transpose_batch(const TransposeJobs& jobs, hipStream_t st) {
+  if (jobs.n <= 0) return hipSuccess;
+  int maxt = 1;
+  for (int j = 0; j < jobs.n; ++j) {
+    const int t = (int)(cdiv(jobs.job[j].rows, 32) * cdiv(jobs.job[j].cols, 32));
+    maxt = t > maxt ? t : maxt;
+  }
+  hipLaunchKernelGGL(k_transpose, dim3(maxt, jobs.n), dim3(256), 0, st, jobs);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// edge init (GNN.py:85-87) after the node-level GEMM P = x @ W0[:, :F]^T
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_edge_init(const float* __restrict__ P,
+                                                   const int* __restrict__ src_s,
+                                                   const float* __restrict__ e_s, int Fe, int Fep,
+                                                   const float* __restrict__ w0eT,
+                                                   const float* __restrict__ b0, int64_t E, int H,
+                                                   int Hp, int act, float* __restrict__ h0,
+                                                   float* __restrict__ pre0) {
+  const int C4 = Hp >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= E * C4) return;
+  const int64_t i = t / C4;
+  const int c = (int)(t - i * C4);
+  const int n = 4 * c;
+  float4 z = *reinterpret_cast<const float4*>(P + (int64_t)src_s[i] * Hp + n);
+  z.x += b0[min(n, H - 1)];
+  z.y += b0[min(n + 1, H - 1)];
+  z.z += b0[min(n + 2, H - 1)];
+  z.w += b0[min(n + 3, H - 1)];
+  const float* er = e_s + i * Fep;
+  for (int q = 0; q < Fe; ++q) {
+    const float ev = er[q];
+    const float4 w = *reinterpret_cast<const float4*>(w0eT + (int64_t)q * Hp + n);
+    z.x += ev * w.x;
+    z.y += ev * w.y;
+    z.z += ev * w.z;
+    z.w += ev * w.w;
+  }
+  const int64_t o = i * Hp + n;
+  if (pre0) *reinterpret_cast<float4*>(pre0 + o) = z;
+  float4 h;
+  h.x = act_fwd(z.x, act);
+  h.y = act_fwd(z.y, act);
+  h.z = act_fwd(z.z, act);
+  h.w = act_fwd(z.w, act);
+  *reinterpret_cast<float4*>(h0 + o) = h;
+}
+
+hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int Fe, int Fep,
+                         const float* w0eT, const float* b0, int64_t E, int H, int Hp, int act,
+                         float* h0, float* pre0, hipStream_t st) {
+  if (E <= 0) return hipSuccess;
+  const int64_t tot = E * (Hp / 4);
+  hipLaunchKernelGGL(k_edge_init, dim3(cdiv(tot, 256)), dim3(256), 0, st, P, src_s, e_s, Fe, Fep,
+                     w0eT, b0, E, H, Hp, act, h0, pre0);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// add-pool + ffn head (GNN.py:110): one workgroup per graph
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pool_head(const float* __restrict__ hn, int Hp,
+                                                   const int* __restrict__ gptr, int H,
+                                                   const float* __restrict__ wf,
+                                                   const float* __restrict__ bf,
+                                                   float* __restrict__ g, float* __restrict__ y) {
+  const int b = blockIdx.x;
+  const int v0 = gptr[b], v1 = gptr[b + 1];
+  float dot = 0.f;
+  for (int n = threadIdx.x; n < H; n += blockDim.x) {
+    float s = 0.f;
+    for (int v = v0; v < v1; ++v) s += hn[(int64_t)v * Hp + n];
+    g[(int64_t)b * Hp + n] = s;
+    dot += s * wf[n];
+  }
+  __shared__ float red[4];
+  dot = wave_sum(dot);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dot;
+  __syncthreads();
+  if (threadIdx.x == 0) y[b] = (red[0] + red[1]) + (red[2] + red[3]) + bf[0];
+}
+
+hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
+                         const float* wf, const float* bf, float* g, float* y, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pool_head, dim3(B), dim3(256), 0, st, hn, Hp, gptr, H, wf, bf, g, y);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// backward: head
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ dy,
+                                                  const float* __restrict__ g,
+                                                  const float* __restrict__ wf, int64_t B, int H,
+                                                  int Hp, float* __restrict__ dg,
+                                                  float* __restrict__ dwf,
+                                                  float* __restrict__ dbf) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n < H) {
+    const float w = wf[n];
+    float acc = 0.f;
+    for (int64_t b = 0; b < B; ++b) {
+      const float d = dy[b];
+      acc += d * g[b * Hp + n];
+      dg[b * Hp + n] = d * w;
+    }
+    dwf[n] = acc;
+  }
+  if (blockIdx.x == 0) {
+    float s = 0.f;
+    for (int64_t b = threadIdx.x; b < B; b += blockDim.x) s += dy[b];
+    __shared__ float red[4];
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) dbf[0] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B, int H, int Hp,
+                    float* dg, float* dwf, float* dbf, hipStream_t st) {
+  hipLaunchKernelGGL(k_head_bwd, dim3(cdiv(H, 256)), dim3(256), 0, st, dy, g, wf, B, H, Hp, dg,
+                     dwf, dbf);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dg,
+                                                     const int* __restrict__ node_graph,
+                                                     const float* __restrict__ hn,
+                                                     const float* __restrict__ zn, int64_t N,
+                                                     int Hp, int act, float* __restrict__ dzn) {
+  const int C4 = Hp >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * C4) return;
+  const int64_t v = t / C4;
+  const int c = (int)(t - v * C4);
+  const int64_t o = v * Hp + 4 * c;
+  const float4 d = *reinterpret_cast<const float4*>(dg + (int64_t)node_graph[v] * Hp + 4 * c);
+  float4 r;
+  if (act == ACT_RELU) {
+    const float4 h = *reinterpret_cast<const float4*>(hn + o);
+    r.x = h.x > 0.f ? d.x : 0.f;
+    r.y = h.y > 0.f ? d.y : 0.f;
+    r.z = h.z > 0.f ? d.z : 0.f;
+    r.w = h.w > 0.f ? d.w : 0.f;
+  } else {
+    const float4 z = *reinterpret_cast<const float4*>(zn + o);
+    r.x = d.x * act_grad(z.x, act);
+    r.y = d.y * act_grad(z.y, act);
+    r.z = d.z * act_grad(z.z, act);
+    r.w = d.w * act_grad(z.w, act);
+  }
+  *reinterpret_cast<float4*>(dzn + o) = r;
+}
+
+hipError_t readout_act_bwd(const float* dg, const int* node_graph, const float* hn,
+                           const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
+                           hipStream_t st) {
+  (void)H;
+  if (N <= 0) return hipSuccess;
+  const int64_t tot = N * (Hp / 4);
+  hipLaunchKernelGGL(k_readout_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dg, node_graph, hn, zn,
+                     N, Hp, act, dzn);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// backward: D-MPNN layer activation / skip / dropout (GNN.py:94-102 reversed)
+// ------------------------------------------------------------------------------------------
+int layer_act_bwd_blocks(int64_t E, int Hp) { return (int)cdiv(E * (Hp / 4), 256); }
+
+__global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
+  const int C4 = a.Hp >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  float dsig = 0.f;
+  if (t < a.E * C4) {
+    const int64_t i = t / C4;
+    const int c = (int)(t - i * C4);
+    const int n = 4 * c;
+    const int64_t o = i * a.Hp + n;
+    float4 dh;
+    if (a.first) {
+      dh = *reinterpret_cast<const float4*>(a.ds + (int64_t)a.dst_s[i] * a.Hp + n);
+    } else {
+      dh = f4sub(*reinterpret_cast<const float4*>(a.da + (int64_t)a.dst_s[i] * a.Hp + n),
+                 *reinterpret_cast<const float4*>(a.dm + (int64_t)a.rev_s[i] * a.Hp + n));
+    }
+    float d[4] = {dh.x, dh.y, dh.z, dh.w};
+    if (a.act == ACT_RELU) {
+      const float4 hv = *reinterpret_cast<const float4*>(a.hnext + o);
+      const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
+    } else {
+      const float4 zv = *reinterpret_cast<const float4*>(a.pre + o);
+      const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float m = a.scale;
+        if (a.thresh && n + k < a.H)
+          m = drop_keep(a.seed, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
+                                                                                        : 0.f;
+        d[k] = d[k] * m * act_grad(zz[k], a.act);
+      }
+    }
+    const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
+    *reinterpret_cast<float4*>(a.dpre + o) = dp;
+    const float sg = a.sigma ? a.sigma[0] : 1.f;
+    float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
+    acc.x += sg * dp.x;
+    acc.y += sg * dp.y;
+    acc.z += sg * dp.z;
+    acc.w += sg * dp.w;
+    *reinterpret_cast<float4*>(a.dh0 + o) = acc;
+    if (a.dsig_part) {
+      const float4 h0 = *reinterpret_cast<const float4*>(a.h0 + o);
+      const float hz[4] = {h0.x, h0.y, h0.z, h0.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        if (n + k < a.H) dsig += d[k] * hz[k];
+    }
+  }
+  if (a.dsig_part) {
+    __shared__ float red[4];
+    dsig = wave_sum(dsig);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dsig;
+    __syncthreads();
+    if (threadIdx.x == 0) a.dsig_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+hipError_t layer_act_bwd(const LayerBwdArgs& a, int* nblocks_out, hipStream_t st) {
+  const int nb = layer_act_bwd_blocks(a.E, a.Hp);
+  if (nblocks_out) *nblocks_out = nb;
+  if (nb <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_layer_bwd, dim3(nb), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_edge_init_bwd(
+    const float* __restrict__ dh0, const float* __restrict__ da, const float* __restrict__ dm,
+    const int* __restrict__ dst_s, const int* __restrict__ rev_s, const float* __restrict__ h0,
+    const float* __restrict__ pre0, int64_t E, int Hp, int act, float* __restrict__ dpre0) {
+  const int C4 = Hp >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= E * C4) return;
+  const int64_t i = t / C4;
+  const int n = 4 * (int)(t - i * C4);
+  const int64_t o = i * Hp + n;
+  float4 d = f4add(*reinterpret_cast<const float4*>(dh0 + o),
+                   f4sub(*reinterpret_cast<const float4*>(da + (int64_t)dst_s[i] * Hp + n),
+                         *reinterpret_cast<const float4*>(dm + (int64_t)rev_s[i] * Hp + n)));
+  if (act == ACT_RELU) {
+    const float4 h = *reinterpret_cast<const float4*>(h0 + o);
+    d.x = h.x > 0.f ? d.x : 0.f;
+    d.y = h.y > 0.f ? d.y : 0.f;
+    d.z = h.z > 0.f ? d.z : 0.f;
+    d.w = h.w > 0.f ? d.w : 0.f;
+  } else {
+    const float4 z = *reinterpret_cast<const float4*>(pre0 + o);
+    d.x *= act_grad(z.x, act);
+    d.y *= act_grad(z.y, act);
+    d.z *= act_grad(z.z, act);
+    d.w *= act_grad(z.w, act);
+  }
+  *reinterpret_cast<float4*>(dpre0 + o) = d;
+}
+
+hipError_t edge_init_bwd(const float* dh0, const float* da, const float* dm, const int* dst_s,
+                         const int* rev_s, const float* h0, const float* pre0, int64_t E, int H,
+                         int Hp, int act, float* dpre0, hipStream_t st) {
+  (void)H;
+  if (E <= 0) return hipSuccess;
+  const int64_t tot = E * (Hp / 4);
+  hipLaunchKernelGGL(k_edge_init_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dh0, da, dm, dst_s,
+                     rev_s, h0, pre0, E, Hp, act, dpre0);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// deterministic split-K reduction of weight-gradient slabs
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ slab,
+                                                      const float* __restrict__ bslab, int splits,
+                                                      int Nout, int Kout, float* __restrict__ dst,
+                                                      int64_t ld_dst, int64_t col_off,
+                                                      float* __restrict__ bias_dst) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t nk = (int64_t)Nout * Kout;
+  if (t < nk) {
+    const int64_t n = t / Kout, k = t - n * Kout;
+    float s = 0.f;
+    for (int p = 0; p < splits; ++p) s += slab[(int64_t)p * nk + t];
+    dst[n * ld_dst + col_off + k] = s;
+  } else if (bias_dst && t < nk + Nout) {
+    const int64_t n = t - nk;
+    float s = 0.f;
+    for (int p = 0; p < splits; ++p) s += bslab[(int64_t)p * Nout + n];
+    bias_dst[n] = s;
+  }
+}
+
+hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
+                        float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
+                        hipStream_t st) {
+  const int64_t tot = (int64_t)Nout * Kout + (bias_dst ? Nout : 0);
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(tot, 256)), dim3(256), 0, st, slab, bslab, splits,
+                     Nout, Kout, dst, ld_dst, col_off, bias_dst);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int nb,
+                                                         ScalarReduceJobs jobs) {
+  const int j = blockIdx.x;
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[(int64_t)j * nb + b];
+  __shared__ float red[4];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) jobs.out[j][0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+hipError_t reduce_partials(const float* part, int nb, const ScalarReduceJobs& jobs,
+                           hipStream_t st) {
+  if (jobs.n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_reduce_partials, dim3(jobs.n), dim3(256), 0, st, part, nb, jobs);
+  return hipGetLastError();
+}
+
+}  // namespace cgr

@@ -1,0 +1,90 @@
+// Host wrappers of the non-GEMM kernels (kernels.hip).  All enqueue on `st`, no sync.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cgr {
+
+// out[s, :w] = sum_{j in [ptr[s], ptr[s+1])} vals[idx ? idx[j] : j, :w]
+hipError_t segment_sum(const float* vals, int64_t ldv, const int* idx, const int* ptr,
+                       int64_t nseg, int64_t width, float* out, int64_t ldo, hipStream_t st);
+
+struct TransposeJob {
+  const float* src;  // [rows, ld_src], columns [col_off, col_off + cols)
+  int64_t ld_src;
+  int64_t col_off;
+  float* dst;  // [cols, ld_dst]
+  int64_t ld_dst;
+  int rows, cols;
+};
+constexpr int kMaxTransposeJobs = 40;
+struct TransposeJobs {
+  TransposeJob job[kMaxTransposeJobs];
+  int n;
+};
+hipError_t transpose_batch(const TransposeJobs& jobs, hipStream_t st);
+
+// h0 = act(P[src_s] + e_s @ W0e^T + b0) ; pre0 stored if non-null
+hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int Fe, int Fep,
+                         const float* w0eT, const float* b0, int64_t E, int H, int Hp, int act,
+                         float* h0, float* pre0, hipStream_t st);
+
+// g[b] = sum_{v in graph b} hn[v];  y[b] = g[b] . wf + bf
+hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
+                         const float* wf, const float* bf, float* g, float* y, hipStream_t st);
+
+// dg[b] = dy[b] wf ; dwf = sum_b dy[b] g[b] ; dbf = sum_b dy[b]
+hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B, int H, int Hp,
+                    float* dg, float* dwf, float* dbf, hipStream_t st);
+
+// dzn[v] = dg[graph(v)] * act'(zn[v])   (ReLU: hn > 0)
+hipError_t readout_act_bwd(const float* dg, const int* node_graph, const float* hn,
+                           const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
+                           hipStream_t st);
+
+struct LayerBwdArgs {
+  // dh_{l+1}: first layer (l == D-1): ds[dst_s[i]], else da[dst_s[i]] - dm[rev_s[i]]
+  const float* ds;
+  const float* da;
+  const float* dm;
+  const int* dst_s;
+  const int* rev_s;
+  const float* hnext;  // h_{l+1} (ReLU mask)
+  const float* pre;    // pre_{l} (non-ReLU)
+  const float* h0;
+  const float* sigma;  // skip weight (nullptr -> 1)
+  uint64_t seed;
+  uint32_t thresh;
+  float scale;
+  int layer;
+  int act;
+  int first;
+  int64_t E;
+  int H, Hp;
+  float* dpre;
+  float* dh0;         // written (first) or accumulated
+  float* dsig_part;   // [gridDim] partial sums of dpre*h0 (nullable)
+};
+hipError_t layer_act_bwd(const LayerBwdArgs& a, int* nblocks_out, hipStream_t st);
+int layer_act_bwd_blocks(int64_t E, int Hp);
+
+// dpre0 = (dh0 + da[dst_s] - dm[rev_s]) * act'(pre0)   (ReLU: h0 > 0)
+hipError_t edge_init_bwd(const float* dh0, const float* da, const float* dm, const int* dst_s,
+                         const int* rev_s, const float* h0, const float* pre0, int64_t E, int H,
+                         int Hp, int act, float* dpre0, hipStream_t st);
+
+// dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
+hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
+                        float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
+                        hipStream_t st);
+
+// out[j][0] = sum_b part[j * nb + b]   for j < njobs (scalar grads of skip weights)
+struct ScalarReduceJobs {
+  float* out[64];
+  int n;
+};
+hipError_t reduce_partials(const float* part, int nb, const ScalarReduceJobs& jobs,
+                           hipStream_t st);
+
+}  // namespace cgr

@@ -1,0 +1,167 @@
+/*
+ * cgr_mpnn3d.h - C ABI of the MI355X-native CGR-MPNN-3D D-MPNN hot path (libcgr_mpnn3d.so).
+ *
+ * The reference (tobjec/CGR-MPNN-3D @ 2025-02-27) is pure Python; its hot path is the
+ * ``GNN`` / ``DMPNNConv`` pair in ``cgr_mpnn_3D/models/GNN.py`` plus two PyTorch-Geometric
+ * sum-scatters.  Each entry point below replaces one of those interfaces (file:line cited) and is
+ * bound from Python by ``cgr_mpnn_3D/_amd/native.py`` (ctypes), which keeps the reference's
+ * ``nn.Module`` surface so ``train.py`` / ``test.py`` drop in unchanged.
+ *
+ * Conventions
+ *   - plain pointers and sizes only; every pointer argument named d_* / listed as "device" is
+ *     device memory on the current HIP device; `stream` is a hipStream_t passed as void*
+ *     (NULL = legacy default stream).  Calls only enqueue work: no allocation, no host sync, so
+ *     they can be captured into a hipGraph.
+ *   - fp32 data, row-major; int64 graph indices exactly as PyG produces them.
+ *   - parameters / gradients are passed as a table of device pointers in the reference
+ *     ``state_dict`` order (see CGR_PARAM_*), each tensor contiguous in the reference layout
+ *     (nn.Linear weight = [out, in]).
+ *   - return 0 on success, a CGR_ERR_* code otherwise; cgr_last_error() describes the failure
+ *     (thread-local).  Python raises RuntimeError with that text.
+ */
+#ifndef CGR_MPNN3D_H
+#define CGR_MPNN3D_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGR_ABI_VERSION 1
+#define CGR_MAX_DEPTH 32
+
+enum cgr_status {
+  CGR_OK = 0,
+  CGR_ERR_INVALID_ARGUMENT = 1,
+  CGR_ERR_HIP = 2,
+  CGR_ERR_UNSUPPORTED = 3,
+};
+
+/* activation_fn of GNN.__init__ (GNN.py:21); train.py:284-292 offers F.relu / F.silu / F.gelu */
+enum cgr_activation { CGR_ACT_RELU = 0, CGR_ACT_SILU = 1, CGR_ACT_GELU = 2 };
+
+/* GNN.__init__(num_node_features, num_edge_features, depth, hidden_sizes, dropout_ps,
+ *              activation_fn, aggr="add", pooling_fn=global_add_pool, use_learnable_skip)
+ * (GNN.py:14-74).  The math of the reference requires one uniform hidden size (GNN.py:53-65). */
+typedef struct cgr_gnn_config {
+  int32_t num_node_features; /* F  (78 CGR + 768 MACE for CGR-MPNN-3D) */
+  int32_t num_edge_features; /* Fe (14), may be 0 */
+  int32_t hidden;            /* H  = hidden_sizes[i] for all i */
+  int32_t depth;             /* D  (1 .. CGR_MAX_DEPTH) */
+  int32_t activation;        /* enum cgr_activation */
+  int32_t learnable_skip;    /* use_learnable_skip (GNN.py:71-74, :94-97) */
+} cgr_gnn_config;
+
+/* One collated batch, the fields GNN.forward reads from a PyG Batch (GNN.py:77-82). */
+typedef struct cgr_batch {
+  const float* x;            /* device [N, F]  data.x */
+  const int64_t* edge_index; /* device [2, E]  data.edge_index (row 0 = src, row 1 = dst) */
+  const float* edge_attr;    /* device [E, Fe] data.edge_attr (NULL allowed when Fe == 0) */
+  const int64_t* batch;      /* device [N]     data.batch, sorted graph id per node; NULL = one
+                                graph (global_add_pool(h, None), GNN.py:110) */
+  const int64_t* graph_ptr;  /* device [B+1]   Batch.ptr node offsets, or NULL (derived from
+                                `batch` on the device) */
+  int64_t num_nodes;         /* N */
+  int64_t num_edges;         /* E (even: reverse edge of e is e ^ 1, GNN.py:136-138) */
+  int64_t num_graphs;        /* B (1 when batch == NULL) */
+} cgr_batch;
+
+/* Parameter table order = reference state_dict order (GNN.py:53-74):
+ *   [0] edge_init.weight [H, F+Fe]   [1] edge_init.bias [H]
+ *   [2+2l] convs.l.lin.weight [H, H] [3+2l] convs.l.lin.bias [H]          l = 0..D-1
+ *   [2+2D] edge_to_node.weight [H, F+H]  [3+2D] edge_to_node.bias [H]
+ *   [4+2D] ffn.weight [1, H]         [5+2D] ffn.bias [1]
+ *   [6+2D+l] skip_weights.l []       (only when learnable_skip)                              */
+#define CGR_PARAM_EDGE_INIT_W 0
+#define CGR_PARAM_EDGE_INIT_B 1
+#define CGR_PARAM_CONV_W(l) (2 + 2 * (l))
+#define CGR_PARAM_CONV_B(l) (3 + 2 * (l))
+#define CGR_PARAM_E2N_W(D) (2 + 2 * (D))
+#define CGR_PARAM_E2N_B(D) (3 + 2 * (D))
+#define CGR_PARAM_FFN_W(D) (4 + 2 * (D))
+#define CGR_PARAM_FFN_B(D) (5 + 2 * (D))
+#define CGR_PARAM_SKIP(D, l) (6 + 2 * (D) + (l))
+
+int cgr_abi_version(void);
+const char* cgr_last_error(void);
+
+/* number of entries of the parameter / gradient tables for `cfg` */
+int cgr_gnn_num_params(const cgr_gnn_config* cfg);
+
+/* Bytes of the per-forward arena (index bookkeeping + activations saved for backward) and of the
+ * backward scratch workspace.  The caller owns both (e.g. torch.empty(uint8) on the device). */
+int64_t cgr_gnn_arena_bytes(const cgr_gnn_config* cfg, int64_t num_nodes, int64_t num_edges,
+                            int64_t num_graphs);
+int64_t cgr_gnn_workspace_bytes(const cgr_gnn_config* cfg, int64_t num_nodes, int64_t num_edges,
+                                int64_t num_graphs);
+
+/* Byte offset of a named arena buffer (introspection for tests/debugging).  Names: "status",
+ * "perm", "src_s", "dst_s", "rev_s", "src_list", "dst_ptr", "src_ptr", "graph_ptr",
+ * "node_graph", "e_s", "P", "h", "a", "pre", "zn", "hn", "g"; `index` selects the layer for
+ * "h" / "a" / "pre".  Returns -1 for an unknown or absent buffer. */
+int64_t cgr_gnn_arena_offset(const cgr_gnn_config* cfg, int64_t num_nodes, int64_t num_edges,
+                             int64_t num_graphs, const char* name, int32_t index);
+
+/* Index bookkeeping only (also run by cgr_gnn_forward): stable dst-sorted edge order, reverse
+ * edge map, src/dst CSR, graph node ranges.  Replaces the implicit index handling of
+ * GNN.py:85,132-138 and PyG's scatter/pool indexing (GNN.py:110,134). */
+int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* batch, void* arena, void* stream);
+
+/* GNN.forward(data) -> [B] (GNN.py:76-110): edge init, `depth` fused D-MPNN layers
+ * (gather -> MFMA GEMM -> bias/skip/act/dropout epilogue -> segmented reduce), edge->node
+ * readout, add-pool and ffn.  Dropout (GNN.py:100-102) is applied when `training` != 0 and
+ * dropout_p[l] > 0, from a counter-based RNG keyed by `seed`.  Fills `arena` with what
+ * cgr_gnn_backward needs.  `y` device [B]. */
+int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params,
+                    const cgr_batch* batch, const float* dropout_p, uint64_t seed,
+                    int32_t training, void* arena, float* y, void* stream);
+
+/* Reverse mode of cgr_gnn_forward (what autograd runs for the reference: GNN.py:76-145 under
+ * loss.backward(), trainer.py:142-143).  `dy` device [B] = dLoss/dy; writes every parameter
+ * gradient into the table `grads` (same order and shapes as `params`, overwritten, not
+ * accumulated).  `arena` must come from the matching forward call; `workspace` is scratch. */
+int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params,
+                     const cgr_batch* batch, const float* dropout_p, uint64_t seed,
+                     int32_t training, const void* arena, const float* dy, float* const* grads,
+                     void* workspace, void* stream);
+
+/* Segmented sum, the sum-scatter primitive of the path (PyG propagate aggr="add", GNN.py:134;
+ * global_add_pool, GNN.py:110) over a CSR: out[s, :] = sum_{j in [seg_ptr[s], seg_ptr[s+1])}
+ * values[index ? index[j] : j, :].  width = row length in floats; ld_* = row strides (floats).
+ * Deterministic (fixed summation order, no atomics). */
+int cgr_segment_sum(const float* values, int64_t ld_values, const int32_t* index,
+                    const int32_t* seg_ptr, int64_t num_segments, int64_t width, float* out,
+                    int64_t ld_out, void* stream);
+
+/* DMPNNConv.forward(edge_index, edge_attr) -> (a, h') (GNN.py:131-141), in the caller's edge
+ * order: a[v] = sum_{dst(e)=v} h[e] (dim_size = N), h'[e] = (a[src(e)] - h[e^1]) W^T + b.
+ * `scratch` needs cgr_dmpnn_conv_scratch_bytes(N, E, H). */
+int64_t cgr_dmpnn_conv_scratch_bytes(int64_t num_nodes, int64_t num_edges, int64_t hidden);
+int cgr_dmpnn_conv_forward(const int64_t* edge_index, int64_t num_nodes, int64_t num_edges,
+                           const float* h, int64_t hidden, const float* weight, const float* bias,
+                           float* a_out, float* h_out, void* scratch, void* stream);
+/* Reverse mode of cgr_dmpnn_conv_forward given dL/da (may be NULL) and dL/dh' (may be NULL):
+ * writes dL/dh [E,H], dL/dW [H,H], dL/db [H].  `scratch` must hold the forward's bookkeeping
+ * (same scratch buffer, untouched since the forward) plus cgr_dmpnn_conv_scratch_bytes. */
+int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t num_nodes, int64_t num_edges,
+                            const float* h, int64_t hidden, const float* weight,
+                            const float* grad_a, const float* grad_h_out, float* grad_h,
+                            float* grad_weight, float* grad_bias, void* scratch, void* stream);
+
+/* Instrumentation (no reference counterpart): per-kernel-class device time measured with HIP
+ * events recorded on the launch stream around every launch of cgr_gnn_forward/_backward.
+ * Off by default; do not enable while capturing a graph.  cgr_profile_collect() waits for the
+ * recorded events; cgr_profile_report() writes "name count total_ms" lines and returns the
+ * buffer size needed. */
+int cgr_profile_enable(int32_t on);
+int cgr_profile_collect(void);
+void cgr_profile_reset(void);
+int64_t cgr_profile_report(char* buf, int64_t len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CGR_MPNN3D_H */

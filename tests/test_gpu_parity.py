@@ -1,0 +1,456 @@
+"""GPU parity: the HIP path (through the C-ABI) vs the reference golden vectors and the oracle.
+
+Tolerances (north_star: fp32 outputs within 1e-4 relative; index bookkeeping bit-exact):
+  * predictions:  |y - y_ref| <= 1e-4 * |y_ref| + 1e-6 * max|y_ref|
+  * gradients:    max|g - g_ref| <= 1e-4 * max|g_ref|   (per parameter tensor)
+  * integers:     exact equality
+"""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden_cases, load_golden
+
+from cgr_mpnn_3D._amd.debug import ArenaRun
+from cgr_mpnn_3D._amd.synth import TorchBatch, make_batch
+from cgr_mpnn_3D.models.GNN import GNN
+from oracle import dmpnn_numpy as on
+
+pytestmark = pytest.mark.gpu
+
+ACT = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu}
+Y_RTOL = 1e-4
+G_RTOL = 1e-4
+
+
+def assert_y_close(y, ref):
+    y = np.asarray(y, np.float64)
+    ref = np.asarray(ref, np.float64)
+    tol = Y_RTOL * np.abs(ref) + 1e-6 * np.abs(ref).max()
+    bad = np.abs(y - ref) > tol
+    assert not bad.any(), f"max abs err {np.abs(y - ref).max():.3e} at {np.argmax(np.abs(y-ref))}"
+
+
+def assert_g_close(g, ref, name=""):
+    g = np.asarray(g, np.float64)
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(g - ref).max() / (np.abs(ref).max() + 1e-30)
+    assert err <= G_RTOL, f"{name}: rel err {err:.3e}"
+
+
+def model_from_golden(z, meta, dev, dropout=None):
+    D, H = meta["depth"], meta["hidden"]
+    m = GNN(meta["num_node_features"], meta["num_edge_features"], depth=D, hidden_sizes=[H] * D,
+            dropout_ps=[dropout if dropout is not None else meta["eval_dropout"]] * D,
+            activation_fn=ACT[meta["act"]], use_learnable_skip=meta["skip"])
+    sd = {k[2:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("p_")}
+    m.load_state_dict(sd)
+    return m.to(dev)
+
+
+def batch_from_golden(z, meta, dev):
+    batch = None if meta["batch_none"] else torch.from_numpy(z["in_batch"]).to(dev)
+    return TorchBatch(torch.from_numpy(z["in_x"]).to(dev),
+                      torch.from_numpy(z["in_edge_index"]).to(dev),
+                      torch.from_numpy(z["in_edge_attr"]).to(dev), batch,
+                      None if meta["batch_none"] else torch.from_numpy(z["in_ptr"]).to(dev),
+                      torch.from_numpy(z["in_y"]).to(dev))
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_forward_matches_reference_golden(case, cuda_device):
+    z, meta = load_golden(case)
+    m = model_from_golden(z, meta, cuda_device)
+    m.eval()
+    with torch.no_grad():
+        y = m(batch_from_golden(z, meta, cuda_device))
+    assert tuple(y.shape) == tuple(z["out_y_eval"].shape)
+    assert_y_close(y.cpu().numpy(), z["out_y_eval"])
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_gradients_match_reference_golden(case, cuda_device):
+    z, meta = load_golden(case)
+    m = model_from_golden(z, meta, cuda_device, dropout=0.0)
+    m.train()
+    data = batch_from_golden(z, meta, cuda_device)
+    pred = m(data)
+    loss = torch.nn.MSELoss(reduction="sum")(pred, data.y.view_as(pred))
+    loss.backward()
+    assert abs(loss.item() - float(z["out_loss"])) <= 1e-4 * abs(float(z["out_loss"]))
+    for k, p in m.named_parameters():
+        assert_g_close(p.grad.cpu().numpy(), z["g_" + k], k)
+
+
+def _cfg_tuple(F_, Fe, H, D, act, skip):
+    return (F_, Fe, H, D, {"relu": 0, "silu": 1, "gelu": 2}[act], skip)
+
+
+def _graph_prep_check(b, dev, use_ptr=True, batch_none=False):
+    x = torch.from_numpy(b.x).to(dev)
+    ei = torch.from_numpy(b.edge_index).to(dev)
+    ea = torch.from_numpy(b.edge_attr).to(dev)
+    batch = None if batch_none else torch.from_numpy(b.batch).to(dev)
+    ptr = torch.from_numpy(b.ptr).to(dev) if (use_ptr and not batch_none) else None
+    B = 1 if batch_none else b.num_graphs
+    H, D = 16, 1
+    F_, Fe = x.shape[1], ea.shape[1]
+    torch.manual_seed(0)
+    m = GNN(F_, Fe, depth=D, hidden_sizes=[H]).to(dev)
+    run = ArenaRun(_cfg_tuple(F_, Fe, H, D, "relu", False), x, ei, ea, batch, ptr, B,
+                   [p.detach() for p in m.native_parameters()])
+    torch.cuda.synchronize()
+    N, E = x.shape[0], ei.shape[1]
+    g = on.graph_prep(b.edge_index, N, None if batch_none else b.batch, B)
+    for name, n in (("perm", E), ("src_s", E), ("dst_s", E), ("rev_s", E), ("src_list", E),
+                    ("dst_ptr", N + 1), ("src_ptr", N + 1), ("graph_ptr", B + 1)):
+        got = run.ints(name, n).cpu().numpy()
+        np.testing.assert_array_equal(got, g[name], err_msg=name)
+    ng = run.ints("node_graph", N).cpu().numpy()
+    np.testing.assert_array_equal(ng, np.zeros(N) if batch_none else b.batch)
+    assert run.ints("status", 1).item() == 0
+    # sorted, zero padded edge features
+    es = run.floats("e_s", E, cols=(Fe + 3) // 4 * 4).cpu().numpy()
+    np.testing.assert_array_equal(es[:, :Fe], b.edge_attr[g["perm"]])
+    assert not es[:, Fe:].any()
+
+
+def test_graph_prep_bit_exact_cfg2(cuda_device):
+    _graph_prep_check(make_batch(256, seed=1234), cuda_device)
+
+
+def test_graph_prep_bit_exact_ragged_batch_vector_only(cuda_device):
+    _graph_prep_check(make_batch(37, n_atoms=25, n_bonds=30, n_mace=0, seed=5, n_atoms_jitter=20),
+                      cuda_device, use_ptr=False)
+
+
+def test_graph_prep_bit_exact_stress_graphs(cuda_device):
+    _graph_prep_check(make_batch(8, n_atoms=200, n_bonds=400, n_mace=0, seed=6), cuda_device)
+
+
+def test_graph_prep_single_graph_batch_none(cuda_device):
+    _graph_prep_check(make_batch(1, n_atoms=10, n_bonds=12, n_mace=0, seed=7), cuda_device,
+                      batch_none=True)
+
+
+def _oracle_compare(b, H, D, act, skip, dev, seed=0):
+    F_, Fe = b.x.shape[1], b.edge_attr.shape[1]
+    torch.manual_seed(seed)
+    m = GNN(F_, Fe, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D, activation_fn=ACT[act],
+            use_learnable_skip=skip)
+    if skip:
+        with torch.no_grad():
+            for i, w in enumerate(m.skip_weights):
+                w.fill_(0.5 + 0.25 * i)
+    sd = {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
+    m = m.to(dev).train()
+    data = b.to_torch(dev)
+    pred = m(data)
+    loss = torch.nn.MSELoss(reduction="sum")(pred, data.y)
+    loss.backward()
+    loss_o, y_o, g_o = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, D, act,
+                                         skip, num_graphs=b.num_graphs)
+    assert_y_close(pred.detach().cpu().numpy(), y_o)
+    for k, p in m.named_parameters():
+        assert_g_close(p.grad.cpu().numpy(), g_o[k], k)
+
+
+def test_cfg2_shape_vs_oracle(cuda_device):
+    # the real cfg2 widths (F = 846, Fe = 14, H = 400, D = 4) on 32 reactions (oracle in seconds)
+    _oracle_compare(make_batch(32, seed=21), 400, 4, "relu", False, cuda_device)
+
+
+def test_cfg5_shape_vs_oracle(cuda_device):
+    # depth 6, hidden 512, learnable skip, MACE concat (BASELINE cfg5 with the list padded to 6)
+    _oracle_compare(make_batch(16, seed=22), 512, 6, "relu", True, cuda_device)
+
+
+@pytest.mark.parametrize("act", ["silu", "gelu"])
+def test_smooth_activations_vs_oracle(act, cuda_device):
+    _oracle_compare(make_batch(12, n_atoms=30, n_bonds=34, n_mace=40, seed=23), 128, 3, act, True,
+                    cuda_device)
+
+
+def test_stress_graphs_vs_oracle(cuda_device):
+    # cfg4-shaped reactions (200 atoms / 800 directed edges), 4 of them
+    _oracle_compare(make_batch(4, n_atoms=200, n_bonds=400, n_mace=64, seed=24), 400, 4, "relu",
+                    False, cuda_device)
+
+
+def test_odd_hidden_size_vs_oracle(cuda_device):
+    # H not a multiple of 4 (padded rows) and F odd (scalar x loads)
+    _oracle_compare(make_batch(6, n_atoms=14, n_bonds=16, n_mace=7, seed=25), 37, 2, "silu", True,
+                    cuda_device)
+
+
+# ---------------------------------------------------------------------------------------------
+# full-size (BASELINE cfg2 / cfg4) size-independent properties
+# ---------------------------------------------------------------------------------------------
+def _run(m, data):
+    m.zero_grad(set_to_none=True)
+    pred = m(data)
+    loss = torch.nn.MSELoss(reduction="sum")(pred, data.y)
+    loss.backward()
+    return pred.detach().clone(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+
+def _slice_batch(b, g0, g1):
+    v0, v1 = int(b.ptr[g0]), int(b.ptr[g1])
+    emask = (b.edge_index[0] >= v0) & (b.edge_index[0] < v1)
+    from cgr_mpnn_3D._amd.synth import RxnBatch
+
+    return RxnBatch(x=b.x[v0:v1].copy(), edge_index=(b.edge_index[:, emask] - v0).copy(),
+                    edge_attr=b.edge_attr[emask].copy(), batch=b.batch[v0:v1] - g0,
+                    ptr=b.ptr[g0:g1 + 1] - v0, y=b.y[g0:g1].copy())
+
+
+@pytest.mark.parametrize("cfg", ["cfg2", "cfg4"])
+def test_full_size_determinism_independence_additivity(cfg, cuda_device):
+    from cgr_mpnn_3D._amd.synth import CONFIGS
+
+    c = CONFIGS[cfg]
+    nb = c["num_graphs"] if cfg == "cfg2" else 64
+    b = make_batch(nb, n_atoms=c["n_atoms"], n_bonds=c["n_bonds"], n_mace=c["n_mace"], seed=31)
+    torch.manual_seed(0)
+    D, H = c["depth"], c["hidden"]
+    m = GNN(b.x.shape[1], 14, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D).to(cuda_device)
+    m.train()
+    data = b.to_torch(cuda_device)
+    y1, g1 = _run(m, data)
+    y2, g2 = _run(m, data)
+    # bitwise reproducible (no atomics in any reduction)
+    assert torch.equal(y1, y2)
+    for k in g1:
+        assert torch.equal(g1[k], g2[k]), k
+    # graphs are independent: predictions of two halves == prediction of the whole batch
+    half = nb // 2
+    ya, ga = _run(m, _slice_batch(b, 0, half).to_torch(cuda_device))
+    yb, gb = _run(m, _slice_batch(b, half, nb).to_torch(cuda_device))
+    assert_y_close(torch.cat([ya, yb]).cpu().numpy(), y1.cpu().numpy())
+    # the summed loss's gradient is additive over disjoint graph sets
+    for k in g1:
+        assert_g_close((ga[k] + gb[k]).cpu().numpy(), g1[k].cpu().numpy(), k)
+
+
+def test_last_graph_isolated_node_strict_mode(cuda_device):
+    from cgr_mpnn_3D._amd import config
+
+    z, _ = load_golden("isolated_last_node")
+    torch.manual_seed(7)
+    m = GNN(z["in_x"].shape[1], z["in_edge_attr"].shape[1], depth=2, hidden_sizes=[16, 16],
+            dropout_ps=[0.0, 0.0]).to(cuda_device).eval()
+    data = TorchBatch(*(torch.from_numpy(z[k]).to(cuda_device) for k in
+                        ("in_x", "in_edge_index", "in_edge_attr", "in_batch", "in_ptr")))
+    old = config.strict
+    config.strict = True
+    try:
+        with pytest.raises(RuntimeError):  # what the reference raises (golden ref_error)
+            m(data)
+    finally:
+        config.strict = old
+    with torch.no_grad():
+        y = m(data)  # default mode: well-defined result with dim_size = num_nodes
+    assert torch.isfinite(y).all()
+
+
+def test_out_of_range_edge_index_reported_in_strict_mode(cuda_device):
+    from cgr_mpnn_3D._amd import config
+
+    b = make_batch(3, n_atoms=8, n_bonds=8, n_mace=0, seed=3)
+    b.edge_index[1, 5] = b.x.shape[0] + 7
+    m = GNN(78, 14, depth=1, hidden_sizes=[8]).to(cuda_device).eval()
+    old = config.strict
+    config.strict = True
+    try:
+        with pytest.raises((IndexError, RuntimeError)):
+            m(b.to_torch(cuda_device))
+    finally:
+        config.strict = old
+
+
+# ---------------------------------------------------------------------------------------------
+# dropout (train mode): counter-based RNG mask recovered from the saved activations
+# ---------------------------------------------------------------------------------------------
+def test_dropout_matches_oracle_with_recovered_mask(cuda_device):
+    b = make_batch(16, n_atoms=30, n_bonds=30, n_mace=20, seed=41)
+    F_, Fe, H, D, p = b.x.shape[1], 14, 96, 3, 0.25
+    torch.manual_seed(1)
+    m = GNN(F_, Fe, depth=D, hidden_sizes=[H] * D, activation_fn=F.silu).to(cuda_device)
+    params = [q.detach() for q in m.native_parameters()]
+    data = b.to_torch(cuda_device)
+    run = ArenaRun(_cfg_tuple(F_, Fe, H, D, "silu", False), data.x, data.edge_index,
+                   data.edge_attr, data.batch, data.ptr, b.num_graphs, params,
+                   dropout_ps=[p] * D, seed=1234567, training=True)
+    torch.cuda.synchronize()
+    E = data.edge_index.shape[1]
+    perm = run.ints("perm", E).long().cpu().numpy()
+    masks = []
+    for l in range(D):
+        pre = run.floats("pre", E, index=l + 1).cpu().numpy()
+        h = run.floats("h", E, index=l + 1).cpu().numpy()
+        keep_sorted = (h != 0).astype(np.float64)
+        assert np.all(keep_sorted[np.abs(pre) > 1e-3] == (h[np.abs(pre) > 1e-3] != 0))
+        mask = np.empty_like(keep_sorted)
+        mask[perm] = keep_sorted  # back to the caller's edge order
+        rate = 1.0 - mask.mean()
+        assert abs(rate - p) < 0.01, rate
+        masks.append(mask)
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    y_o, cache = on.forward(sd, b.x, b.edge_index, b.edge_attr, b.batch, D, "silu",
+                            dropout_masks=masks, dropout_ps=[p] * D)
+    assert_y_close(run.y.cpu().numpy(), y_o)
+    dy = torch.randn(b.num_graphs, device=cuda_device)
+    grads = run.backward(dy, params)
+    g_o = on.backward(sd, cache, dy.cpu().numpy())
+    names = [k for k, _ in m.named_parameters()]
+    for k, g in zip(names, grads):
+        assert_g_close(g.cpu().numpy(), g_o[k], k)
+    # same seed -> same mask; different seed -> different mask
+    run2 = ArenaRun(_cfg_tuple(F_, Fe, H, D, "silu", False), data.x, data.edge_index,
+                    data.edge_attr, data.batch, data.ptr, b.num_graphs, params,
+                    dropout_ps=[p] * D, seed=1234567, training=True)
+    run3 = ArenaRun(_cfg_tuple(F_, Fe, H, D, "silu", False), data.x, data.edge_index,
+                    data.edge_attr, data.batch, data.ptr, b.num_graphs, params,
+                    dropout_ps=[p] * D, seed=7654321, training=True)
+    assert torch.equal(run.y, run2.y) and not torch.equal(run.y, run3.y)
+
+
+def test_relu_dropout_backward_consistent(cuda_device):
+    b = make_batch(8, n_atoms=20, n_bonds=22, n_mace=0, seed=42)
+    torch.manual_seed(2)
+    m = GNN(78, 14, depth=2, hidden_sizes=[64, 64], dropout_ps=[0.5, 0.1]).to(cuda_device).train()
+    data = b.to_torch(cuda_device)
+    torch.manual_seed(99)
+    y = m(data)
+    y.sum().backward()
+    for _, q in m.named_parameters():
+        assert torch.isfinite(q.grad).all()
+    m.eval()
+    with torch.no_grad():
+        ye = m(data)
+    assert not torch.allclose(y.detach(), ye)
+
+
+# ---------------------------------------------------------------------------------------------
+# the scatter-add primitive and the standalone DMPNNConv
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("width,ld", [(400, 400), (37, 37), (64, 80), (3, 5)])
+@pytest.mark.parametrize("gather", [False, True])
+def test_segment_sum_api(width, ld, gather, cuda_device):
+    import ctypes
+
+    from cgr_mpnn_3D._amd import native
+
+    lib = native.load()
+    rng = np.random.default_rng(width + ld)
+    nseg, rows = 300, 900
+    counts = rng.integers(0, 7, size=nseg)
+    counts[-1] = rows - counts[:-1].sum() if counts[:-1].sum() < rows else 0
+    ptr = np.zeros(nseg + 1, np.int32)
+    ptr[1:] = np.cumsum(counts)
+    total = int(ptr[-1])
+    vals = rng.standard_normal((max(rows, total), ld)).astype(np.float32)
+    idx = rng.permutation(vals.shape[0])[:total].astype(np.int32) if gather else None
+    exp = np.zeros((nseg, width), np.float64)
+    for s in range(nseg):
+        rr = range(ptr[s], ptr[s + 1])
+        rows_ = [idx[j] for j in rr] if gather else list(rr)
+        if rows_:
+            exp[s] = vals[rows_, :width].astype(np.float64).sum(0)
+    dv = torch.from_numpy(vals).to(cuda_device)
+    dp = torch.from_numpy(ptr).to(cuda_device)
+    di = torch.from_numpy(idx).to(cuda_device) if gather else None
+    out = torch.zeros(nseg, ld, device=cuda_device)
+    native.check(lib.cgr_segment_sum(native.ptr(dv), ld, native.ptr(di), native.ptr(dp), nseg,
+                                     width, native.ptr(out), ld,
+                                     native.stream_ptr(cuda_device)))
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(out.cpu().numpy()[:, :width], exp, rtol=1e-5, atol=1e-5)
+    assert not out.cpu().numpy()[:, width:].any()  # never writes past `width`
+
+
+@pytest.mark.parametrize("H", [32, 45])
+def test_dmpnn_conv_standalone_vs_torch_cpu(H, cuda_device):
+    from cgr_mpnn_3D.models.GNN import DMPNNConv
+
+    b = make_batch(5, n_atoms=11, n_bonds=13, n_mace=0, seed=H)
+    E, N = b.edge_index.shape[1], b.x.shape[0]
+    torch.manual_seed(H)
+    conv = DMPNNConv(H)
+    h = torch.randn(E, H)
+    ga = torch.randn(N, H)
+    gh = torch.randn(E, H)
+    # CPU reference of GNN.py:131-141 (torch autograd)
+    hr = h.clone().requires_grad_(True)
+    wr = conv.lin.weight.detach().clone().requires_grad_(True)
+    br = conv.lin.bias.detach().clone().requires_grad_(True)
+    ei = torch.from_numpy(b.edge_index)
+    a_ref = torch.zeros(N, H).index_add(0, ei[1], hr)
+    rev = torch.flip(hr.view(E // 2, 2, H), dims=[1]).reshape(E, H)
+    out_ref = F.linear(a_ref[ei[0]] - rev, wr, br)
+    (a_ref * ga).sum().backward(retain_graph=True)
+    (out_ref * gh).sum().backward()
+    convd = conv.to(cuda_device)
+    hd = h.to(cuda_device).requires_grad_(True)
+    a, out = convd(ei.to(cuda_device), hd)
+    ((a * ga.to(cuda_device)).sum() + (out * gh.to(cuda_device)).sum()).backward()
+    torch.testing.assert_close(a.detach().cpu(), a_ref.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out.detach().cpu(), out_ref.detach(), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(hd.grad.cpu(), hr.grad, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(convd.lin.weight.grad.cpu(), wr.grad, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(convd.lin.bias.grad.cpu(), br.grad, rtol=1e-4, atol=1e-3)
+
+
+# ---------------------------------------------------------------------------------------------
+# training-loop drop-in (trainer.py:138-147 pattern) and graph capture
+# ---------------------------------------------------------------------------------------------
+def test_trainer_loop_reduces_loss(cuda_device):
+    b = make_batch(64, n_atoms=30, n_bonds=30, n_mace=32, seed=51)
+    torch.manual_seed(0)
+    m = GNN(b.x.shape[1], 14, depth=3, hidden_sizes=[64] * 3).to(cuda_device)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, amsgrad=True)
+    loss_fn = torch.nn.MSELoss(reduction="sum")
+    data = b.to_torch(cuda_device)
+    m.train()
+    losses = []
+    for _ in range(30):
+        opt.zero_grad()
+        pred = m(data)
+        loss = loss_fn(pred, data.y)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    assert losses[-1] < 0.5 * losses[0]
+
+
+def test_cuda_graph_capture_replays_fwd_bwd(cuda_device):
+    b = make_batch(32, seed=61)
+    torch.manual_seed(0)
+    m = GNN(b.x.shape[1], 14, depth=4, hidden_sizes=[400] * 4, dropout_ps=[0.0] * 4)
+    m = m.to(cuda_device).train()
+    data = b.to_torch(cuda_device)
+    params = list(m.parameters())
+
+    def step():
+        pred = m(data)
+        loss = torch.nn.MSELoss(reduction="sum")(pred, data.y)
+        gs = torch.autograd.grad(loss, params)
+        return pred, gs
+
+    eager_pred, eager_g = step()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        gp, gg = step()
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(gp, eager_pred)
+    for a, c in zip(gg, eager_g):
+        assert torch.equal(a, c)

@@ -1,0 +1,71 @@
+"""CPU: the drop-in module keeps the reference's surface (GNN.py:8-145)."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden_cases, load_golden
+
+from cgr_mpnn_3D.models.GNN import GNN, DMPNNConv, global_add_pool
+
+
+@pytest.mark.parametrize("case", [c for c in golden_cases()])
+def test_state_dict_keys_shapes_and_seeded_init_match_reference(case):
+    z, meta = load_golden(case)
+    D, H = meta["depth"], meta["hidden"]
+    torch.manual_seed(1000 + len(case))  # the seed make_golden.py used before ref.GNN(...)
+    m = GNN(meta["num_node_features"], meta["num_edge_features"], depth=D, hidden_sizes=[H] * D,
+            dropout_ps=[meta["eval_dropout"]] * D,
+            activation_fn={"relu": F.relu, "silu": F.silu, "gelu": F.gelu}[meta["act"]],
+            use_learnable_skip=meta["skip"])
+    sd = m.state_dict()
+    ref_keys = [k[2:] for k in z.files if k.startswith("p_")]
+    assert set(sd.keys()) == set(ref_keys)
+    for k in ref_keys:
+        assert tuple(sd[k].shape) == tuple(z["p_" + k].shape), k
+        if not k.startswith("skip_weights"):  # make_golden overwrote sigma after init
+            np.testing.assert_array_equal(sd[k].numpy(), z["p_" + k], err_msg=k)
+
+
+def test_defaults_and_attributes():
+    m = GNN(10, 3)
+    assert m.depth == 3 and m.hidden_sizes == [300] * 3 and m.dropout_ps == [0.02] * 3
+    assert m.activation_fn is F.relu and m.pooling_fn is global_add_pool
+    assert not m.use_learnable_skip and not hasattr(m, "skip_weights")
+    assert isinstance(m.convs[0], DMPNNConv) and m.convs[0].lin.in_features == 300
+    assert m.edge_init.in_features == 13 and m.edge_to_node.in_features == 310
+    assert m.ffn.out_features == 1
+
+
+def test_short_hidden_sizes_raise_index_error_like_reference():
+    # BASELINE cfg5 literal: depth 6 with five hidden sizes -> IndexError (GNN.py:59-60)
+    with pytest.raises(IndexError):
+        GNN(846, 14, depth=6, hidden_sizes=[512] * 5)
+
+
+def test_cpu_tensors_raise_no_fallback():
+    from cgr_mpnn_3D._amd.synth import make_batch
+
+    b = make_batch(2, n_atoms=6, n_bonds=6, n_mace=0).to_torch()
+    m = GNN(78, 14, depth=2, hidden_sizes=[16, 16])
+    with pytest.raises(RuntimeError, match="GPU"):
+        m(b)
+
+
+def test_global_add_pool_semantics():
+    x = torch.arange(12.0).view(6, 2)
+    b = torch.tensor([0, 0, 1, 1, 1, 2])
+    torch.testing.assert_close(global_add_pool(x, b),
+                               torch.tensor([[2.0, 4.0], [18.0, 21.0], [10.0, 11.0]]))
+    assert global_add_pool(x, None).shape == (1, 2)
+
+
+def test_pickle_roundtrip_keeps_class_paths(tmp_path):
+    m = GNN(8, 2, depth=2, hidden_sizes=[4, 4], use_learnable_skip=True)
+    p = tmp_path / "m.pth"
+    torch.save(m, p)
+    m2 = torch.load(p, weights_only=False)  # our own file (trainer.py:208 saves full modules)
+    assert type(m2).__module__ == "cgr_mpnn_3D.models.GNN"
+    for (k1, v1), (k2, v2) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert k1 == k2 and torch.equal(v1, v2)

@@ -1,0 +1,120 @@
+"""CPU: pin the oracle (oracle/) against golden vectors produced by the reference GNN.py itself."""
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import golden_cases, load_golden
+from oracle import dmpnn_numpy as on
+from oracle.dmpnn_torch import TorchRestatement, random_state_dict
+
+ACT = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu}
+CASES = golden_cases()
+
+
+def _inputs(z, meta):
+    params = {k[2:]: z[k] for k in z.files if k.startswith("p_")}
+    batch = None if meta["batch_none"] else z["in_batch"]
+    return params, batch
+
+
+def rel_err(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / (np.max(np.abs(b)) + 1e-30))
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_numpy_oracle_forward_matches_reference(case):
+    z, meta = load_golden(case)
+    params, batch = _inputs(z, meta)
+    y, _ = on.forward(params, z["in_x"], z["in_edge_index"], z["in_edge_attr"], batch,
+                      meta["depth"], meta["act"], meta["skip"], num_graphs=len(z["in_ptr"]) - 1)
+    ref = z["out_y_eval"]
+    assert y.shape == ref.shape
+    np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_numpy_oracle_gradients_match_reference(case):
+    z, meta = load_golden(case)
+    params, batch = _inputs(z, meta)
+    loss, y, grads = on.loss_and_grads(params, z["in_x"], z["in_edge_index"], z["in_edge_attr"],
+                                       batch, z["in_y"], meta["depth"], meta["act"],
+                                       meta["skip"], num_graphs=len(z["in_ptr"]) - 1)
+    assert abs(loss - float(z["out_loss"])) <= 1e-5 * abs(float(z["out_loss"]))
+    ref_keys = {k[2:] for k in z.files if k.startswith("g_")}
+    assert set(grads) == ref_keys
+    for k in ref_keys:
+        assert rel_err(grads[k], z["g_" + k]) < 1e-5, k
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_torch_restatement_is_bitwise_reference(case):
+    z, meta = load_golden(case)
+    params, batch = _inputs(z, meta)
+    m = TorchRestatement(params, meta["depth"], ACT[meta["act"]], meta["skip"])
+    m.eval()
+    with torch.no_grad():
+        y = m(torch.from_numpy(z["in_x"]), torch.from_numpy(z["in_edge_index"]),
+              torch.from_numpy(z["in_edge_attr"]),
+              None if batch is None else torch.from_numpy(batch))
+    np.testing.assert_array_equal(y.numpy(), z["out_y_eval"])
+
+
+def test_reference_error_on_isolated_last_node_recorded():
+    z, _ = load_golden("isolated_last_node")
+    assert str(z["ref_error"]) == "RuntimeError"
+
+
+def test_graph_prep_oracle_invariants():
+    from cgr_mpnn_3D._amd.synth import make_batch
+
+    b = make_batch(5, n_atoms=12, n_bonds=15, n_mace=0, seed=3, n_atoms_jitter=4)
+    N, E = b.x.shape[0], b.edge_index.shape[1]
+    g = on.graph_prep(b.edge_index, N, b.batch, b.num_graphs)
+    src, dst = b.edge_index
+    # stable dst order
+    assert np.all(np.diff(g["dst_s"]) >= 0)
+    assert np.array_equal(g["dst_s"], dst[g["perm"]])
+    # reverse map is an involution and points at the reverse pair e ^ 1
+    assert np.array_equal(g["rev_s"][g["rev_s"]], np.arange(E))
+    assert np.array_equal(g["perm"][g["rev_s"]], g["perm"] ^ 1)
+    assert np.array_equal(g["src_s"][g["rev_s"]], g["dst_s"])
+    # CSR offsets
+    assert g["dst_ptr"][-1] == E and g["src_ptr"][-1] == E
+    assert np.array_equal(g["graph_ptr"], b.ptr)
+    for v in range(N):
+        seg = g["src_list"][g["src_ptr"][v]:g["src_ptr"][v + 1]]
+        assert np.all(g["src_s"][seg] == v) and np.all(np.diff(seg) > 0)
+
+
+def test_oracle_learnable_skip_gradient_finite_difference():
+    """Independent check of the hand-derived backward on a tiny graph (sigma and W_0)."""
+    from cgr_mpnn_3D._amd.synth import make_batch
+
+    b = make_batch(2, n_atoms=5, n_bonds=6, n_mace=3, seed=9)
+    sd = {k: v.numpy().astype(np.float64) for k, v in
+          random_state_dict(b.x.shape[1], 14, 6, 2, learnable_skip=True, seed=1).items()}
+    sd["skip_weights.0"] = np.asarray(0.7)
+    for act in ("relu", "silu", "gelu"):
+        _, _, grads = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, 2, act,
+                                        True)
+        for key, idx in (("skip_weights.0", ()), ("edge_init.weight", (1, 3)),
+                         ("convs.1.lin.weight", (2, 4))):
+            eps = 1e-6
+            p = dict(sd)
+            arr = np.array(sd[key], dtype=np.float64)
+            arr[idx] += eps
+            p[key] = arr
+            lp, _, _ = on.loss_and_grads(p, b.x, b.edge_index, b.edge_attr, b.batch, b.y, 2, act,
+                                         True)
+            arr2 = np.array(sd[key], dtype=np.float64)
+            arr2[idx] -= eps
+            p[key] = arr2
+            lm, _, _ = on.loss_and_grads(p, b.x, b.edge_index, b.edge_attr, b.batch, b.y, 2, act,
+                                         True)
+            fd = (lp - lm) / (2 * eps)
+            an = float(np.asarray(grads[key])[idx])
+            assert abs(fd - an) <= 1e-5 * max(1.0, abs(fd)), (act, key, fd, an)
