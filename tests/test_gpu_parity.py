@@ -437,7 +437,9 @@ def test_cuda_graph_capture_replays_fwd_bwd(cuda_device):
         pred = m(data)
         loss = torch.nn.MSELoss(reduction="sum")(pred, data.y)
         gs = torch.autograd.grad(loss, params)
-        return pred, gs
+        # return no tensor that keeps this iteration's autograd graph alive: a live graph from
+        # the eager step makes capture reuse its AccumulateGrad nodes on another stream
+        return pred.detach(), gs
 
     eager_pred, eager_g = step()
     s = torch.cuda.Stream()
