@@ -180,7 +180,7 @@ def main():
     loss_fn = torch.nn.MSELoss(reduction="sum")
 
     def step():
-        opt.zero_grad(set_to_none=False)
+        opt.zero_grad(set_to_none=True)
         loss = loss_fn(model(data), data.y)
         loss.backward()
         opt.step()

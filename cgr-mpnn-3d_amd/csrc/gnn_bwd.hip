@@ -80,7 +80,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     ProfScope _p("head_readout_bwd", st);
     HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, dg,
                      grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], st));
-    HIP_RET(readout_act_bwd(dg, iv.node_graph, fv.hn, fv.zn, N, H, Hp, d.act, dzn, st));
+    HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H, Hp,
+                            d.act, dzn, st));
   }
   {
     const int vx = vec_for(b->x, F, F);

@@ -188,80 +188,96 @@ hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, in
 }
 
 // ------------------------------------------------------------------------------------------
-// backward: head
+// backward: ffn head + add-pool + edge_to_node activation
+//   dwf[n] = sum_b dy[b] g[b, n] ; dbf = sum_b dy[b]            (k_head_bwd, column reduction)
+//   dzn[v, n] = dy[graph(v)] * wf[n] * act'(zn[v, n])           (k_readout_bwd; dg never stored)
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_head_bwd(const float* __restrict__ dy,
-                                                  const float* __restrict__ g,
-                                                  const float* __restrict__ wf, int64_t B, int H,
-                                                  int Hp, float* __restrict__ dg,
-                                                  float* __restrict__ dwf,
-                                                  float* __restrict__ dbf) {
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n < H) {
-    const float w = wf[n];
-    float acc = 0.f;
-    for (int64_t b = 0; b < B; ++b) {
-      const float d = dy[b];
-      acc += d * g[b * Hp + n];
-      dg[b * Hp + n] = d * w;
-    }
-    dwf[n] = acc;
+__global__ __launch_bounds__(1024) void k_head_bwd(const float* __restrict__ dy,
+                                                   const float* __restrict__ g, int64_t B, int H,
+                                                   int Hp, float* __restrict__ dwf,
+                                                   float* __restrict__ dbf) {
+  // block = 64 columns x 16 row phases
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + tx;
+  float acc = 0.f, sdy = 0.f;
+  for (int64_t b = ty; b < B; b += 16) {
+    const float d = dy[b];
+    if (n < H) acc += d * g[b * Hp + n];
+    sdy += d;
+  }
+  __shared__ float red[16][65];
+  red[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][tx];
+    if (n < H) dwf[n] = s;
   }
   if (blockIdx.x == 0) {
-    float s = 0.f;
-    for (int64_t b = threadIdx.x; b < B; b += blockDim.x) s += dy[b];
-    __shared__ float red[4];
-    s = wave_sum(s);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
-    if (threadIdx.x == 0) dbf[0] = (red[0] + red[1]) + (red[2] + red[3]);
+    red[ty][tx] = sdy;  // every tx of a row phase summed the same dy values
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += red[k][0];
+      dbf[0] = s;
+    }
   }
 }
 
 hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B, int H, int Hp,
                     float* dg, float* dwf, float* dbf, hipStream_t st) {
-  hipLaunchKernelGGL(k_head_bwd, dim3(cdiv(H, 256)), dim3(256), 0, st, dy, g, wf, B, H, Hp, dg,
-                     dwf, dbf);
+  (void)wf;
+  (void)dg;
+  hipLaunchKernelGGL(k_head_bwd, dim3(cdiv(H, 64)), dim3(1024), 0, st, dy, g, B, H, Hp, dwf, dbf);
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dg,
+__global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dy,
+                                                     const float* __restrict__ wf,
                                                      const int* __restrict__ node_graph,
                                                      const float* __restrict__ hn,
                                                      const float* __restrict__ zn, int64_t N,
-                                                     int Hp, int act, float* __restrict__ dzn) {
+                                                     int H, int Hp, int act,
+                                                     float* __restrict__ dzn) {
   const int C4 = Hp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * C4) return;
   const int64_t v = t / C4;
   const int c = (int)(t - v * C4);
-  const int64_t o = v * Hp + 4 * c;
-  const float4 d = *reinterpret_cast<const float4*>(dg + (int64_t)node_graph[v] * Hp + 4 * c);
+  const int n = 4 * c;
+  const int64_t o = v * Hp + n;
+  const float d = dy[node_graph[v]];
   float4 r;
+  r.x = d * wf[min(n, H - 1)];
+  r.y = d * wf[min(n + 1, H - 1)];
+  r.z = d * wf[min(n + 2, H - 1)];
+  r.w = d * wf[min(n + 3, H - 1)];
   if (act == ACT_RELU) {
     const float4 h = *reinterpret_cast<const float4*>(hn + o);
-    r.x = h.x > 0.f ? d.x : 0.f;
-    r.y = h.y > 0.f ? d.y : 0.f;
-    r.z = h.z > 0.f ? d.z : 0.f;
-    r.w = h.w > 0.f ? d.w : 0.f;
+    r.x = h.x > 0.f ? r.x : 0.f;
+    r.y = h.y > 0.f ? r.y : 0.f;
+    r.z = h.z > 0.f ? r.z : 0.f;
+    r.w = h.w > 0.f ? r.w : 0.f;
   } else {
     const float4 z = *reinterpret_cast<const float4*>(zn + o);
-    r.x = d.x * act_grad(z.x, act);
-    r.y = d.y * act_grad(z.y, act);
-    r.z = d.z * act_grad(z.z, act);
-    r.w = d.w * act_grad(z.w, act);
+    r.x *= act_grad(z.x, act);
+    r.y *= act_grad(z.y, act);
+    r.z *= act_grad(z.z, act);
+    r.w *= act_grad(z.w, act);
   }
   *reinterpret_cast<float4*>(dzn + o) = r;
 }
 
-hipError_t readout_act_bwd(const float* dg, const int* node_graph, const float* hn,
-                           const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
-                           hipStream_t st) {
-  (void)H;
+hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
+                           const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
+                           float* dzn, hipStream_t st) {
   if (N <= 0) return hipSuccess;
   const int64_t tot = N * (Hp / 4);
-  hipLaunchKernelGGL(k_readout_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dg, node_graph, hn, zn,
-                     N, Hp, act, dzn);
+  hipLaunchKernelGGL(k_readout_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dy, wf, node_graph, hn,
+                     zn, N, H, Hp, act, dzn);
   return hipGetLastError();
 }
 

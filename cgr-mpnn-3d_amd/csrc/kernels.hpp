@@ -34,14 +34,14 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
 hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
                          const float* wf, const float* bf, float* g, float* y, hipStream_t st);
 
-// dg[b] = dy[b] wf ; dwf = sum_b dy[b] g[b] ; dbf = sum_b dy[b]
+// dwf = sum_b dy[b] g[b] ; dbf = sum_b dy[b]   (dg is folded into readout_act_bwd)
 hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B, int H, int Hp,
                     float* dg, float* dwf, float* dbf, hipStream_t st);
 
-// dzn[v] = dg[graph(v)] * act'(zn[v])   (ReLU: hn > 0)
-hipError_t readout_act_bwd(const float* dg, const int* node_graph, const float* hn,
-                           const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
-                           hipStream_t st);
+// dzn[v] = dy[graph(v)] * wf * act'(zn[v])   (ReLU: hn > 0)
+hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
+                           const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
+                           float* dzn, hipStream_t st);
 
 struct LayerBwdArgs {
   // dh_{l+1}: first layer (l == D-1): ds[dst_s[i]], else da[dst_s[i]] - dm[rev_s[i]]
