@@ -53,7 +53,7 @@ constexpr int kTnTargetWorkgroups = 1024;  // ~4 per CU on 256 CUs
 
 inline TnPlan tn_plan(int Nout, int Kout, int R) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
-    return plan_tn<decltype(W)::value, decltype(RN)::value>(Nout, Kout, R, kTnTargetWorkgroups);
+    return plan_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(Nout, Kout, R, kTnTargetWorkgroups);
   });
 }
 

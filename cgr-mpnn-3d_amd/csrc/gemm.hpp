@@ -5,26 +5,31 @@
 //
 //   gemm_nt:  C[m, n] = sum_k A(m, k) * B(n, k)      A rows produced by a *loader* (plain rows,
 //             gathered a[src]-h[rev] rows, or the [x | s] concat), B = rows of a weight matrix
-//             ([out, in] = nn.Linear layout); an *epilogue* functor consumes every C element
-//             (bias / skip / activation / dropout / stores).
+//             ([out, in] = nn.Linear layout); an *epilogue* functor consumes C as float4 row
+//             pieces (bias / skip / activation / dropout / stores).
 //   gemm_tn:  C[n, k] = sum_e A(e, n) * B(e, k)      weight gradients dW = dZ^T Q, reduction over
-//             the (long) edge / node dimension, split over gridDim.z into fp32 partial slabs
-//             (deterministic: a separate kernel sums the slabs in a fixed order).  The k-tile-0
-//             workgroups also emit the column sums of A (= the bias gradient) per split.
+//             the (long) edge / node dimension, split over gridDim.y into fp32 partial slabs
+//             (deterministic: reduce_slabs sums them in a fixed order).  Workgroups of k-tile 0
+//             also emit the column sums of A (= the bias gradient) per split.
 //
-// Tiling (one workgroup = WAVES waves of 64 lanes):
-//   NT: BM = 16*WAVES rows (one 16-row MFMA fragment per wave), BN = 16*RN columns (RN column
-//       fragments per wave, A fragment reused RN times), BK = 16.  H = 400 -> RN = 5 (BN = 80)
-//       tiles the hidden dimension exactly.  LDS tile = [row][4 x float4], chunk c of row r
-//       stored at slot c ^ swz(r): every ds_read_b128 of a fragment is bank-conflict free
-//       (16-lane groups of ds_read_b128, MI355X_MICROARCH.md §LDS).  The MFMA's 4-deep k is
-//       mapped so that lane group g = lane>>4 owns k = 4g..4g+3 of the 16-deep tile: one b128
-//       read feeds four MFMAs.
-//   TN: LDS tiles stay e-major ([16][BM + pad], stride = 16 mod 32 floats) and fragments are read
-//       with conflict-free ds_read_b32 (global loads stay coalesced float4 along n / k).
-//   Double-buffered LDS with register prefetch (global loads for tile k+1 issued before the
-//   MFMAs of tile k, written to the other buffer after them); one barrier per k-tile.
-//   Grid: 1-D, remapped so consecutive tiles of one row panel land on one XCD (shared L2).
+// Tiling (one workgroup = WAVES waves of 64 lanes; RM row / RN column 16x16 fragments per wave):
+//   NT: BM = 16*WAVES*RM, BN = 16*RN (H = 400 -> RN = 5 tiles the hidden dim exactly), BK = 16*KT.
+//       LDS tile = [k16][row][4 x float4], chunk c of row r stored at slot c ^ swz(r): every
+//       ds_read_b128 fragment read is bank-conflict free (PMC SQ_LDS_BANK_CONFLICT = 0).  The
+//       MFMA's 4-deep k is mapped so lane group g = lane>>4 owns k = 4g..4g+3 of a 16-deep slice:
+//       one b128 read feeds four MFMAs.
+//   TN: e-major LDS tiles ([BE][BM + pad], stride == 16 mod 32 floats) read with conflict-free
+//       ds_read_b32; global loads stay coalesced float4 along n / k.
+//   Loads are software-pipelined one k-tile ahead through registers.  Loaders are BRANCH-FREE:
+//   fetch() issues every global load unconditionally from a clamped, in-bounds address and
+//   combine() applies masks / the a[src]-h[rev] subtraction when the tile is written to LDS, so
+//   the compiler's s_waitcnt vmcnt lands after the MFMAs instead of in front of them (with
+//   guarded loads hipcc branched around each load and waited vmcnt(0) per load, serialising the
+//   prefetch: cdna_hip_programming.md §5 trap (c)).  Row state that needs an index load (gathered
+//   rows) is computed one tile earlier still.
+//   Epilogue: accumulators -> LDS [BM][BN+4] -> coalesced float4 rows -> ep.apply4 / slab store.
+//   Grid: 1-D (+ split index for TN), bijective XCD remap so the tiles of one row panel share an
+//   XCD's L2.
 #pragma once
 
 #include "common.hpp"
@@ -41,9 +46,34 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return base + (bid >> 3);
 }
 
+// unconditional VEC-wide loads of elements [k, k+4) of a row; sub-chunks starting at >= K read
+// element 0 instead (always in bounds) and are zeroed later by mask4
+template <int VEC>
+__device__ __forceinline__ float4 fetch4(const float* __restrict__ p, int k, int K) {
+  if constexpr (VEC == 4) {
+    return *reinterpret_cast<const float4*>(p + (k < K ? k : 0));
+  } else if constexpr (VEC == 2) {
+    const float2 u = *reinterpret_cast<const float2*>(p + (k < K ? k : 0));
+    const float2 w = *reinterpret_cast<const float2*>(p + (k + 2 < K ? k + 2 : 0));
+    return make_float4(u.x, u.y, w.x, w.y);
+  } else {
+    return make_float4(p[k < K ? k : 0], p[k + 1 < K ? k + 1 : 0], p[k + 2 < K ? k + 2 : 0],
+                       p[k + 3 < K ? k + 3 : 0]);
+  }
+}
+
+__device__ __forceinline__ float4 mask4(float4 v, bool ok, int k, int K) {
+  v.x = (ok && k < K) ? v.x : 0.f;
+  v.y = (ok && k + 1 < K) ? v.y : 0.f;
+  v.z = (ok && k + 2 < K) ? v.z : 0.f;
+  v.w = (ok && k + 3 < K) ? v.w : 0.f;
+  return v;
+}
+
 // ------------------------------------------------------------------------------------------
-// Row loaders.  Interface: Row row(int r, int limit) ; float4 load(const Row&, int k, int K)
-// returning elements k..k+3 of logical row r (0 beyond K or for r >= limit).
+// Row loaders.  Row row(int r, int limit): per-row state (rows >= limit read row 0, masked);
+// Raw fetch(const Row&, int k, int K): the global loads of elements k..k+3;
+// float4 combine(const Raw&, const Row&, int k, int K): masks / arithmetic (0 beyond K).
 // ------------------------------------------------------------------------------------------
 template <int VEC>
 struct LdPlain {
@@ -51,18 +81,24 @@ struct LdPlain {
   int64_t ld;
   struct Row {
     const float* p;
+    bool ok;
   };
+  typedef float4 Raw;
   __device__ __forceinline__ Row row(int r, int limit) const {
-    return Row{r < limit ? base + (int64_t)r * ld : nullptr};
+    const bool ok = r < limit;
+    return Row{base + (int64_t)(ok ? r : 0) * ld, ok};
   }
-  __device__ __forceinline__ float4 load(const Row& rw, int k, int K) const {
-    if (rw.p == nullptr) return f4zero();
-    return load4<VEC>(rw.p + k, K - k);
+  __device__ __forceinline__ Raw fetch(const Row& rw, int k, int K) const {
+    return fetch4<VEC>(rw.p, k, K);
+  }
+  __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
+    return mask4(v, rw.ok, k, K);
   }
 };
 
-// m[e, :] = a[src[e], :] - h[rev[e], :]   (GNN.py:136-141).  Internal buffers, ld = Hp.
-// REV_XOR: rev[e] = e ^ 1 (caller's original edge order, no index array).
+// m[e, :] = a[src[e], :] - h[rev[e], :]   (GNN.py:136-141).  Internal buffers, ld = Hp (% 4 == 0).
+// REV_XOR: rev[e] = e ^ 1 (caller's original edge order, no index array).  Row keeps the raw
+// indices; addresses are formed in fetch() so the index loads are waited for only there.
 template <bool REV_XOR>
 struct LdGatherDiff {
   const float* a;
@@ -71,21 +107,29 @@ struct LdGatherDiff {
   const int* rev;
   int64_t ld;
   struct Row {
-    const float* pa;
-    const float* ph;
+    int s, r;
+    bool ok;
+  };
+  struct Raw {
+    float4 a, h;
   };
   __device__ __forceinline__ Row row(int r, int limit) const {
-    if (r >= limit) return Row{nullptr, nullptr};
-    const int rv = REV_XOR ? (r ^ 1) : rev[r];
-    return Row{a + (int64_t)src[r] * ld, h + (int64_t)rv * ld};
+    const bool ok = r < limit;
+    const int rr = ok ? r : 0;
+    return Row{src[rr], REV_XOR ? (rr ^ 1) : rev[rr], ok};
   }
-  __device__ __forceinline__ float4 load(const Row& rw, int k, int K) const {
-    if (rw.pa == nullptr) return f4zero();
-    return f4sub(load4_masked_internal(rw.pa + k, K - k), load4_masked_internal(rw.ph + k, K - k));
+  __device__ __forceinline__ Raw fetch(const Row& rw, int k, int K) const {
+    const int kk = k < K ? k : 0;
+    return Raw{*reinterpret_cast<const float4*>(a + (int64_t)rw.s * ld + kk),
+               *reinterpret_cast<const float4*>(h + (int64_t)rw.r * ld + kk)};
+  }
+  __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
+    return mask4(f4sub(v.a, v.h), rw.ok, k, K);
   }
 };
 
-// q[v, :] = [x[v, :F] | s[v, :H]]  (GNN.py:106).  VEC divides F and ld_x.
+// q[v, :] = [x[v, :F] | s[v, :H]]  (GNN.py:106).  VEC divides F and ldx (so no VEC sub-chunk
+// straddles F); s rows are internal (16-byte aligned, ld % 4 == 0).
 template <int VEC>
 struct LdConcat {
   const float* x;
@@ -96,196 +140,298 @@ struct LdConcat {
   struct Row {
     const float* px;
     const float* ps;
+    bool ok;
   };
+  typedef float4 Raw;
   __device__ __forceinline__ Row row(int r, int limit) const {
-    if (r >= limit) return Row{nullptr, nullptr};
-    return Row{x + (int64_t)r * ldx, s + (int64_t)r * lds};
+    const bool ok = r < limit;
+    const int rr = ok ? r : 0;
+    return Row{x + (int64_t)rr * ldx, s + (int64_t)rr * lds, ok};
   }
-  __device__ __forceinline__ float4 load(const Row& rw, int k, int K) const {
-    if (rw.px == nullptr) return f4zero();
-    if (k + 4 <= F) return load4<VEC>(rw.px + k, F - k);
-    if (k >= F) return load4<VEC>(rw.ps + (k - F), K - k);
+  __device__ __forceinline__ Raw fetch(const Row& rw, int k, int K) const {
     float v[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int kk = k + i;
-      v[i] = kk < F ? rw.px[kk] : (kk < K ? rw.ps[kk - F] : 0.f);
+    for (int j = 0; j < 4; j += VEC) {
+      const int kk = k + j;
+      const float* p = kk < F ? rw.px + kk : (kk < K ? rw.ps + (kk - F) : rw.px);
+      if constexpr (VEC == 4) {
+        const float4 u = *reinterpret_cast<const float4*>(p);
+        v[0] = u.x;
+        v[1] = u.y;
+        v[2] = u.z;
+        v[3] = u.w;
+      } else if constexpr (VEC == 2) {
+        const float2 u = *reinterpret_cast<const float2*>(p);
+        v[j] = u.x;
+        v[j + 1] = u.y;
+      } else {
+        v[j] = *p;
+      }
     }
     return make_float4(v[0], v[1], v[2], v[3]);
+  }
+  __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
+    return mask4(v, rw.ok, k, K);
   }
 };
 
 // ------------------------------------------------------------------------------------------
 // NT GEMM
 // ------------------------------------------------------------------------------------------
-template <int WAVES, int RN, class AL, class BL, class EP>
+template <int WAVES, int RM, int RN, int KT>
+struct NTShape {
+  static constexpr int NT = WAVES * 64;
+  static constexpr int BM = WAVES * 16 * RM, BN = RN * 16, BK = 16 * KT;
+  static constexpr int CPR = 4 * KT;  // float4 chunks per row per k-tile
+  static constexpr int ACH = BM * CPR, BCH = BN * CPR;
+  static constexpr int APT = ACH / NT;
+  static constexpr int BPT = (BCH + NT - 1) / NT;
+  static constexpr int LDC = BN + 4;
+  static constexpr int STAGE_F4 = 2 * (ACH + BCH);
+  static constexpr int EPI_F4 = (BM * LDC + 3) / 4;
+  static constexpr int LDS_F4 = STAGE_F4 > EPI_F4 ? STAGE_F4 : EPI_F4;
+  static_assert(ACH % NT == 0, "A chunks per thread must be integral");
+};
+
+template <int WAVES, int RM, int RN, int KT, class AL, class BL, class EP>
 __global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N,
                                                              int K, int tiles_n) {
-  constexpr int BM = WAVES * 16, BN = RN * 16, NT = WAVES * 64;
-  constexpr int BCH = BN * 4;
-  constexpr int BPT = (BCH + NT - 1) / NT;
-  __shared__ float4 As[2][BM * 4];
-  __shared__ float4 Bs[2][BN * 4];
+  using S = NTShape<WAVES, RM, RN, KT>;
+  constexpr int NT = S::NT, BM = S::BM, BN = S::BN, BK = S::BK, CPR = S::CPR;
+  constexpr int ACH = S::ACH, BCH = S::BCH, APT = S::APT, BPT = S::BPT;
+  __shared__ float4 lds[S::LDS_F4];
+  float4* As = lds;
+  float4* Bs = lds + 2 * ACH;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  // staging assignment: A one float4 chunk per thread, B up to BPT chunks
-  const int ar = tid >> 2, ac = tid & 3;
-  const typename AL::Row arow = al.row(m0 + ar, M);
+  typename AL::Row arow[APT];
+  int adst[APT], akof[APT];
+#pragma unroll
+  for (int p = 0; p < APT; ++p) {
+    const int q = tid + p * NT;
+    const int r = q / CPR, kc = q % CPR;
+    arow[p] = al.row(m0 + r, M);
+    akof[p] = kc * 4;
+    adst[p] = ((kc >> 2) * BM + r) * 4 + ((kc & 3) ^ lds_swz(r));
+  }
   typename BL::Row brow[BPT];
-  int bdst[BPT], bcol[BPT];
+  int bdst[BPT], bkof[BPT];
 #pragma unroll
   for (int p = 0; p < BPT; ++p) {
-    const int c = tid + p * NT;
-    const int br = c >> 2, bc = c & 3;
-    bcol[p] = bc * 4;
-    bdst[p] = c < BCH ? br * 4 + (bc ^ lds_swz(br)) : -1;
-    brow[p] = bl.row(c < BCH ? n0 + br : N, N);
+    const int q = tid + p * NT;
+    const int r = q / CPR, kc = q % CPR;
+    const bool in = q < BCH;
+    brow[p] = bl.row(in ? n0 + r : N, N);
+    bkof[p] = kc * 4;
+    bdst[p] = in ? ((kc >> 2) * BN + r) * 4 + ((kc & 3) ^ lds_swz(r)) : -1;
   }
-  const int adst = ar * 4 + (ac ^ lds_swz(ar));
 
-  float4 ra, rb[BPT];
-  const int nk = (K + 15) >> 4;
-
-  floatx4 acc[RN];
+  typename AL::Raw ra[APT];
+  typename BL::Raw rb[BPT];
+  floatx4 acc[RM][RN];
 #pragma unroll
-  for (int j = 0; j < RN; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue
-  ra = al.load(arow, ac * 4, K);
+  for (int i = 0; i < RM; ++i)
 #pragma unroll
-  for (int p = 0; p < BPT; ++p) rb[p] = bl.load(brow[p], bcol[p], K);
-  As[0][adst] = ra;
+    for (int j = 0; j < RN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (K + BK - 1) / BK;
+#pragma unroll
+  for (int p = 0; p < APT; ++p) ra[p] = al.fetch(arow[p], akof[p], K);
+#pragma unroll
+  for (int p = 0; p < BPT; ++p) rb[p] = bl.fetch(brow[p], bkof[p], K);
+#pragma unroll
+  for (int p = 0; p < APT; ++p) As[adst[p]] = al.combine(ra[p], arow[p], akof[p], K);
 #pragma unroll
   for (int p = 0; p < BPT; ++p)
-    if (bdst[p] >= 0) Bs[0][bdst[p]] = rb[p];
+    if (bdst[p] >= 0) Bs[bdst[p]] = bl.combine(rb[p], brow[p], bkof[p], K);
   __syncthreads();
 
   const int fr = lane & 15, fg = lane >> 4;
-  const int aread = (w * 16 + fr) * 4 + (fg ^ lds_swz(fr));
-  int bread[RN];
-#pragma unroll
-  for (int j = 0; j < RN; ++j) bread[j] = (j * 16 + fr) * 4 + (fg ^ lds_swz(fr));
-
+  const int sw = fg ^ lds_swz(fr);
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
+    const int kb = (kt + 1) * BK;
     if (more) {
-      const int kb = (kt + 1) * 16;
-      ra = al.load(arow, kb + ac * 4, K);
 #pragma unroll
-      for (int p = 0; p < BPT; ++p) rb[p] = bl.load(brow[p], kb + bcol[p], K);
+      for (int p = 0; p < APT; ++p) ra[p] = al.fetch(arow[p], kb + akof[p], K);
+#pragma unroll
+      for (int p = 0; p < BPT; ++p) rb[p] = bl.fetch(brow[p], kb + bkof[p], K);
     }
-    const float4 a = As[cur][aread];
-    float4 b[RN];
+    const float4* Ac = As + cur * ACH;
+    const float4* Bc = Bs + cur * BCH;
 #pragma unroll
-    for (int j = 0; j < RN; ++j) b[j] = Bs[cur][bread[j]];
+    for (int c16 = 0; c16 < KT; ++c16) {
+      float4 a[RM], b[RN];
 #pragma unroll
-    for (int j = 0; j < RN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[j].x, acc[j], 0, 0, 0);
+      for (int i = 0; i < RM; ++i) a[i] = Ac[(c16 * BM + w * 16 * RM + i * 16 + fr) * 4 + sw];
 #pragma unroll
-    for (int j = 0; j < RN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[j].y, acc[j], 0, 0, 0);
+      for (int j = 0; j < RN; ++j) b[j] = Bc[(c16 * BN + j * 16 + fr) * 4 + sw];
 #pragma unroll
-    for (int j = 0; j < RN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b[j].z, acc[j], 0, 0, 0);
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int j = 0; j < RN; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b[j].w, acc[j], 0, 0, 0);
+        for (int i = 0; i < RM; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(a[i], s), f4get(b[j], s),
+                                                             acc[i][j], 0, 0, 0);
+    }
     if (more) {
-      As[cur ^ 1][adst] = ra;
+      float4* An = As + (cur ^ 1) * ACH;
+      float4* Bn = Bs + (cur ^ 1) * BCH;
+#pragma unroll
+      for (int p = 0; p < APT; ++p) An[adst[p]] = al.combine(ra[p], arow[p], kb + akof[p], K);
 #pragma unroll
       for (int p = 0; p < BPT; ++p)
-        if (bdst[p] >= 0) Bs[cur ^ 1][bdst[p]] = rb[p];
+        if (bdst[p] >= 0) Bn[bdst[p]] = bl.combine(rb[p], brow[p], kb + bkof[p], K);
     }
     __syncthreads();
   }
 
-  // epilogue: C/D map of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg
-  const int rbase = m0 + w * 16 + fg * 4;
+  // epilogue: accumulators -> LDS [BM][LDC] -> coalesced float4 rows -> ep.apply4
+  float* C = reinterpret_cast<float*>(lds);
 #pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int col = n0 + j * 16 + fr;
+  for (int i = 0; i < RM; ++i)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) ep(rbase + r, col, acc[j][r]);
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(w * 16 * RM + i * 16 + fg * 4 + r) * S::LDC + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+  constexpr int C4 = BN / 4;
+  for (int q = tid; q < BM * C4; q += NT) {
+    const int r = q / C4, c4 = q - r * C4;
+    const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
+    ep.apply4(m0 + r, n0 + 4 * c4, v);
   }
 }
 
-template <int WAVES, int RN, class AL, class BL, class EP>
+template <int WAVES, int RM, int RN, int KT, class AL, class BL, class EP>
 inline hipError_t launch_gemm_nt(const AL& al, const BL& bl, const EP& ep, int M, int N, int K,
                                  hipStream_t st) {
-  constexpr int BM = WAVES * 16, BN = RN * 16;
+  using S = NTShape<WAVES, RM, RN, KT>;
   if (M <= 0 || N <= 0) return hipSuccess;
-  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
-  hipLaunchKernelGGL((gemm_nt_kernel<WAVES, RN, AL, BL, EP>), dim3(tm * tn), dim3(WAVES * 64), 0,
-                     st, al, bl, ep, M, N, K, tn);
+  const int tm = (M + S::BM - 1) / S::BM, tn = (N + S::BN - 1) / S::BN;
+  hipLaunchKernelGGL((gemm_nt_kernel<WAVES, RM, RN, KT, AL, BL, EP>), dim3(tm * tn),
+                     dim3(WAVES * 64), 0, st, al, bl, ep, M, N, K, tn);
   return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
 // TN split-K GEMM (weight gradients)
 // ------------------------------------------------------------------------------------------
-template <int WAVES, int RN, class AL, class BL>
-__global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(AL al, BL bl, float* __restrict__ slab,
-                                                             float* __restrict__ bslab, int Nout,
-                                                             int Kout, int R, int rows_per_split,
-                                                             int tiles_k, int want_bias) {
-  constexpr int BM = WAVES * 16, BN = RN * 16, NT = WAVES * 64;
-  constexpr int SA = BM + (((16 - BM % 32) % 32) + 32) % 32;  // stride == 16 (mod 32)
-  constexpr int SB = BN + (((16 - BN % 32) % 32) + 32) % 32;
-  constexpr int ACH = 16 * BM / 4;  // == NT
-  constexpr int BCH = 16 * BN / 4;
-  constexpr int BPT = (BCH + NT - 1) / NT;
-  static_assert(ACH == NT, "one A chunk per thread");
-  __shared__ float At[2][16 * SA];
-  __shared__ float Bt[2][16 * SB];
+struct TnPlan {
+  int tiles_n, tiles_k, splits, rows_per_split;
+};
+
+template <int WAVES, int RM, int RN, int KT>
+struct TNShape {
+  static constexpr int NT = WAVES * 64;
+  static constexpr int BM = WAVES * 16 * RM, BN = RN * 16, BE = 16 * KT;
+  static constexpr int SA = BM + (((16 - BM % 32) % 32) + 32) % 32;  // == 16 (mod 32)
+  static constexpr int SB = BN + (((16 - BN % 32) % 32) + 32) % 32;
+  static constexpr int ACH = BE * BM / 4, BCH = BE * BN / 4;
+  static constexpr int APT = ACH / NT;
+  static constexpr int BPT = (BCH + NT - 1) / NT;
+  static constexpr int LDC = BN + 4;
+  static constexpr int STAGE_F = 2 * BE * (SA + SB);
+  static constexpr int EPI_F = BM * LDC;
+  static constexpr int LDS_F = STAGE_F > EPI_F ? STAGE_F : EPI_F;
+  static_assert(ACH % NT == 0, "A chunks per thread must be integral");
+};
+
+template <int WAVES, int RM, int RN, int KT, class AL, class BL>
+__global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
+    AL al, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout, int R,
+    int rows_per_split, int tiles_k, int want_bias) {
+  using S = TNShape<WAVES, RM, RN, KT>;
+  constexpr int NT = S::NT, BM = S::BM, BN = S::BN, BE = S::BE, SA = S::SA, SB = S::SB;
+  constexpr int BCH = S::BCH, APT = S::APT, BPT = S::BPT;
+  __shared__ __attribute__((aligned(16))) float lds[S::LDS_F];
+  float* At = lds;
+  float* Bt = lds + 2 * BE * SA;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tiles = gridDim.x;
-  const int tile = xcd_remap(blockIdx.x, tiles);
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tnn = tile / tiles_k, tkk = tile - tnn * tiles_k;
   const int n0 = tnn * BM, k0 = tkk * BN;
   const int split = blockIdx.y;
   const int e_begin = split * rows_per_split;
   const int e_end = min(R, e_begin + rows_per_split);
-  const int nt = e_end > e_begin ? (e_end - e_begin + 15) >> 4 : 0;
+  const int nt = e_end > e_begin ? (e_end - e_begin + BE - 1) / BE : 0;
 
-  const int ae = tid / (BM / 4), ac = tid % (BM / 4);
+  int ae[APT], ac[APT];
+#pragma unroll
+  for (int p = 0; p < APT; ++p) {
+    const int q = tid + p * NT;
+    ae[p] = q / (BM / 4);
+    ac[p] = (q % (BM / 4)) * 4;
+  }
   int be[BPT], bc[BPT];
+  bool bin[BPT];
 #pragma unroll
   for (int p = 0; p < BPT; ++p) {
-    const int c = tid + p * NT;
-    be[p] = c < BCH ? c / (BN / 4) : -1;
-    bc[p] = c < BCH ? c % (BN / 4) : 0;
+    const int q = tid + p * NT;
+    bin[p] = q < BCH;
+    be[p] = bin[p] ? q / (BN / 4) : 0;
+    bc[p] = bin[p] ? (q % (BN / 4)) * 4 : 0;
   }
-
-  float4 ra, rb[BPT];
-  auto gload = [&](int t) {
-    const int e = e_begin + t * 16 + ae;
-    const typename AL::Row r = al.row(e, e_end);
-    ra = al.load(r, n0 + ac * 4, Nout);
+  // rows of the tile to fetch next (computed one tile ahead: index loads have a tile to land)
+  typename AL::Row arow[APT];
+  typename BL::Row brow[BPT];
+  typename AL::Raw ra[APT];
+  typename BL::Raw rb[BPT];
+  auto mkrows = [&](int t) {
+    const int e0 = e_begin + t * BE;
+#pragma unroll
+    for (int p = 0; p < APT; ++p) arow[p] = al.row(e0 + ae[p], e_end);
+#pragma unroll
+    for (int p = 0; p < BPT; ++p) brow[p] = bl.row(e0 + be[p], bin[p] ? e_end : 0);
+  };
+  typename AL::Row arow_f[APT];
+  typename BL::Row brow_f[BPT];
+  auto fetch = [&]() {
+#pragma unroll
+    for (int p = 0; p < APT; ++p) {
+      arow_f[p] = arow[p];
+      ra[p] = al.fetch(arow[p], n0 + ac[p], Nout);
+    }
 #pragma unroll
     for (int p = 0; p < BPT; ++p) {
-      if (be[p] >= 0) {
-        const typename BL::Row rr = bl.row(e_begin + t * 16 + be[p], e_end);
-        rb[p] = bl.load(rr, k0 + bc[p] * 4, Kout);
-      }
+      brow_f[p] = brow[p];
+      rb[p] = bl.fetch(brow[p], k0 + bc[p], Kout);
     }
   };
   auto sstore = [&](int buf) {
-    *reinterpret_cast<float4*>(&At[buf][ae * SA + ac * 4]) = ra;
+    float* Ab = At + buf * BE * SA;
+    float* Bb = Bt + buf * BE * SB;
+#pragma unroll
+    for (int p = 0; p < APT; ++p)
+      *reinterpret_cast<float4*>(&Ab[ae[p] * SA + ac[p]]) =
+          al.combine(ra[p], arow_f[p], n0 + ac[p], Nout);
 #pragma unroll
     for (int p = 0; p < BPT; ++p)
-      if (be[p] >= 0) *reinterpret_cast<float4*>(&Bt[buf][be[p] * SB + bc[p] * 4]) = rb[p];
+      if (bin[p])
+        *reinterpret_cast<float4*>(&Bb[be[p] * SB + bc[p]]) =
+            bl.combine(rb[p], brow_f[p], k0 + bc[p], Kout);
   };
 
-  floatx4 acc[RN];
+  floatx4 acc[RM][RN];
 #pragma unroll
-  for (int j = 0; j < RN; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
   const bool do_bias = want_bias && tkk == 0 && tid < BM;
 
   if (nt > 0) {
-    gload(0);
+    mkrows(0);
+    fetch();
+    mkrows(1);
     sstore(0);
   }
   __syncthreads();
@@ -293,68 +439,89 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(AL al, BL bl, float
   for (int t = 0; t < nt; ++t) {
     const int cur = t & 1;
     const bool more = t + 1 < nt;
-    if (more) gload(t + 1);
+    if (more) {
+      fetch();        // tile t+1, rows prepared during the previous iteration
+      mkrows(t + 2);  // index loads for tile t+2
+    }
+    const float* Ab = At + cur * BE * SA;
+    const float* Bb = Bt + cur * BE * SB;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < 4 * KT; ++s) {
       const int er = 4 * s + fg;
-      const float av = At[cur][er * SA + w * 16 + fr];
+      float av[RM], bv[RN];
 #pragma unroll
-      for (int j = 0; j < RN; ++j) {
-        const float bv = Bt[cur][er * SB + j * 16 + fr];
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[j], 0, 0, 0);
-      }
+      for (int i = 0; i < RM; ++i) av[i] = Ab[er * SA + w * 16 * RM + i * 16 + fr];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bv[j] = Bb[er * SB + j * 16 + fr];
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
     if (do_bias) {
 #pragma unroll
-      for (int e = 0; e < 16; ++e) bsum += At[cur][e * SA + tid];
+      for (int e = 0; e < BE; ++e) bsum += Ab[e * SA + tid];
     }
     if (more) sstore(cur ^ 1);
     __syncthreads();
   }
 
+  float* C = lds;
+#pragma unroll
+  for (int i = 0; i < RM; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        C[(w * 16 * RM + i * 16 + fg * 4 + r) * S::LDC + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
   float* out = slab + (int64_t)split * Nout * Kout;
-  const int rbase = n0 + w * 16 + fg * 4;
-#pragma unroll
-  for (int j = 0; j < RN; ++j) {
-    const int col = k0 + j * 16 + fr;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = rbase + r;
-      if (row < Nout && col < Kout) out[(int64_t)row * Kout + col] = acc[j][r];
+  constexpr int C4 = BN / 4;
+  const bool vec_ok = (Kout & 3) == 0;
+  for (int q = tid; q < BM * C4; q += NT) {
+    const int r = q / C4, c4 = q - r * C4;
+    const int row = n0 + r, col = k0 + 4 * c4;
+    if (row >= Nout || col >= Kout) continue;
+    const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
+    float* o = out + (int64_t)row * Kout + col;
+    if (vec_ok && col + 4 <= Kout) {
+      *reinterpret_cast<float4*>(o) = v;
+    } else {
+      o[0] = v.x;
+      if (col + 1 < Kout) o[1] = v.y;
+      if (col + 2 < Kout) o[2] = v.z;
+      if (col + 3 < Kout) o[3] = v.w;
     }
   }
   if (do_bias && n0 + tid < Nout) bslab[(int64_t)split * Nout + n0 + tid] = bsum;
 }
 
-struct TnPlan {
-  int tiles_n, tiles_k, splits, rows_per_split;
-};
-
-template <int WAVES, int RN>
+template <int WAVES, int RM, int RN, int KT>
 inline TnPlan plan_tn(int Nout, int Kout, int R, int target_wgs) {
-  constexpr int BM = WAVES * 16, BN = RN * 16;
+  using S = TNShape<WAVES, RM, RN, KT>;
   TnPlan p;
-  p.tiles_n = (Nout + BM - 1) / BM;
-  p.tiles_k = (Kout + BN - 1) / BN;
+  p.tiles_n = (Nout + S::BM - 1) / S::BM;
+  p.tiles_k = (Kout + S::BN - 1) / S::BN;
   const int tiles = p.tiles_n * p.tiles_k;
   int splits = (target_wgs + tiles - 1) / tiles;
-  const int max_splits = (R + 63) / 64;  // at least 64 rows (4 k-tiles) per split
+  const int max_splits = (R + 4 * S::BE - 1) / (4 * S::BE);  // >= 4 k-tiles per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int rps = (R + splits - 1) / splits;
-  rps = (rps + 15) / 16 * 16;
+  rps = (rps + S::BE - 1) / S::BE * S::BE;
   p.splits = R > 0 ? (R + rps - 1) / rps : 1;
   p.rows_per_split = rps;
   return p;
 }
 
-template <int WAVES, int RN, class AL, class BL>
+template <int WAVES, int RM, int RN, int KT, class AL, class BL>
 inline hipError_t launch_gemm_tn(const AL& al, const BL& bl, const TnPlan& p, float* slab,
                                  float* bslab, int Nout, int Kout, int R, bool want_bias,
                                  hipStream_t st) {
-  hipLaunchKernelGGL((gemm_tn_kernel<WAVES, RN, AL, BL>), dim3(p.tiles_n * p.tiles_k, p.splits),
-                     dim3(WAVES * 64), 0, st, al, bl, slab, bslab, Nout, Kout, R,
-                     p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
+  hipLaunchKernelGGL((gemm_tn_kernel<WAVES, RM, RN, KT, AL, BL>),
+                     dim3(p.tiles_n * p.tiles_k, p.splits), dim3(WAVES * 64), 0, st, al, bl, slab,
+                     bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
   return hipGetLastError();
 }
 

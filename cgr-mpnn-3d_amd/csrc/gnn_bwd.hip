@@ -30,7 +30,7 @@ static hipError_t tn_and_reduce(const AL& al, const BL& bl, int Nout, int Kout, 
   const TnPlan p = tn_plan(Nout, Kout, R);
   ProfScope _p1("gemm_tn_wgrad", st);
   hipError_t e = with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
-    return launch_gemm_tn<decltype(W)::value, decltype(RN)::value>(al, bl, p, slab, bslab, Nout,
+    return launch_gemm_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(al, bl, p, slab, bslab, Nout,
                                                                    Kout, R, bias_dst != nullptr,
                                                                    st);
   });
@@ -99,7 +99,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dzn, Hp};
       LdPlain<4> bl{wT + D * HHp, Hp};
       EpStore ep{ds, Hp, N, H, nullptr};
-      return launch_gemm_nt<4, decltype(RN)::value>(al, bl, ep, N, H, H, st);
+      return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, N, H, H, st);
     });
     HIP_RET(e);
   }
@@ -150,7 +150,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         LdPlain<4> al{dpre, Hp};
         LdPlain<4> bl{wT + l * HHp, Hp};
         EpStore ep{dm, Hp, E, H, nullptr};
-        return launch_gemm_nt<4, decltype(RN)::value>(al, bl, ep, E, H, H, st);
+        return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H, st);
       });
       HIP_RET(e);
     }

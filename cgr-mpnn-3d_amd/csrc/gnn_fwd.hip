@@ -77,7 +77,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
           LdPlain<decltype(VX)::value> al{b->x, F};
           LdPlain<decltype(VW)::value> bl{W0, F + Fe};
           EpStore ep{fv.P, Hp, N, H, nullptr};
-          return launch_gemm_nt<4, decltype(RN)::value>(al, bl, ep, N, H, F, st);
+          return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, H, F, st);
         });
       });
     });
@@ -112,7 +112,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     hipError_t e = with_vec(vw, [&](auto VW) {
       return with_nt_rn(H, [&](auto RN) {
         LdPlain<decltype(VW)::value> blw{Wl, H};
-        return launch_gemm_nt<4, decltype(RN)::value>(al, blw, ep, E, H, H, st);
+        return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, E, H, H, st);
       });
     });
     HIP_RET(e);
@@ -133,7 +133,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
         return with_nt_rn(H, [&](auto RN) {
           LdConcat<decltype(VX)::value> al{b->x, F, fv.a[D], Hp, F};
           LdPlain<decltype(VW)::value> blw{Wn, F + H};
-          return launch_gemm_nt<4, decltype(RN)::value>(al, blw, ep, N, H, F + H, st);
+          return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, blw, ep, N, H, F + H, st);
         });
       });
     });

@@ -407,6 +407,8 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
   if (t < nk) {
     const int64_t n = t / Kout, k = t - n * Kout;
     float s = 0.f;
+    // fixed summation order (deterministic); unrolled so the loads of 8 splits are in flight
+#pragma unroll 8
     for (int p = 0; p < splits; ++p) s += slab[(int64_t)p * nk + t];
     dst[n * ld_dst + col_off + k] = s;
   } else if (bias_dst && t < nk + Nout) {
