@@ -78,6 +78,7 @@ ArenaLayout arena_layout(const Dims& d) {
   L.e_s = d.Fep ? b.take(4 * E * (size_t)d.Fep) : kNone;
   L.w0eT = d.Fe ? b.take(4 * (size_t)d.Fe * Hp) : kNone;
   L.P = b.take(4 * N * Hp);
+  L.Q = b.take(4 * N * Hp);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
     L.a[l] = l <= d.D ? b.take(4 * N * Hp) : kNone;
@@ -125,6 +126,7 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.e_s = (float*)at(arena, L.e_s);
   f.w0eT = (float*)at(arena, L.w0eT);
   f.P = (float*)at(arena, L.P);
+  f.Q = (float*)at(arena, L.Q);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     f.h[l] = (float*)at(arena, L.h[l]);
     f.a[l] = (float*)at(arena, L.a[l]);
@@ -141,7 +143,8 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   WorkspaceLayout W;
   Bump b;
   const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
-  W.dpre = b.take(4 * E * Hp);
+  W.dpre[0] = b.take(4 * E * Hp);
+  W.dpre[1] = b.take(4 * E * Hp);
   W.dm = b.take(4 * E * Hp);
   W.dh0 = b.take(4 * E * Hp);
   W.da = b.take(4 * N * Hp);
@@ -157,14 +160,20 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     slab = s > slab ? s : slab;
     bslab = bs > bslab ? bs : bslab;
   };
+  // side-stream TN GEMMs (readout, layers, edge features) share one slab; the main-stream TN
+  // (x-part of edge init) runs concurrently with the last of them and gets its own
   acc(d.H, d.F + d.H, d.N);
   acc(d.H, d.H, d.E);
   if (d.Fe > 0) acc(d.H, d.Fe, d.E);
-  if (d.F > 0) acc(d.H, d.F, d.N);
   W.slab_elems = slab;
   W.bslab_elems = bslab;
   W.slab = b.take(4 * slab);
   W.bslab = b.take(4 * bslab);
+  slab = 0;
+  bslab = 0;
+  if (d.F > 0) acc(d.H, d.F, d.N);
+  W.slab2 = b.take(4 * (slab > 0 ? slab : 1));
+  W.bslab2 = b.take(4 * (bslab > 0 ? bslab : 1));
   W.dsig_blocks = layer_act_bwd_blocks(d.E, d.Hp);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
   W.bytes = b.off;
@@ -241,6 +250,7 @@ int64_t cgr_gnn_arena_offset(const cgr_gnn_config* cfg, int64_t N, int64_t E, in
   else if (n == "node_graph") o = L.node_graph;
   else if (n == "e_s") o = L.e_s;
   else if (n == "P") o = L.P;
+  else if (n == "Q") o = L.Q;
   else if (n == "h" && li) o = L.h[index];
   else if (n == "a" && li) o = L.a[index];
   else if (n == "pre" && li) o = L.pre[index];

@@ -101,6 +101,66 @@ struct EpLayer {
   }
 };
 
+// merged x-GEMM output [N, 2H]: columns [0, H) -> P (edge-init half), [H, 2H) -> Q (readout's
+// x-part); both internal [N, ld] buffers.
+struct EpSplit2 {
+  float* P;
+  float* Q;
+  int64_t ld;
+  int M, H;
+  __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
+    if (r >= M || c >= 2 * H) return;
+    if (c + 4 <= H) {
+      *reinterpret_cast<float4*>(P + (int64_t)r * ld + c) = v;
+    } else if (c >= H) {
+      *reinterpret_cast<float4*>(Q + (int64_t)r * ld + (c - H)) = v;  // padding cols don't-care
+    } else {  // straddles H (H % 4 != 0)
+      const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int cc = c + k;
+        if (cc < H) P[(int64_t)r * ld + cc] = e[k];
+        else if (cc < 2 * H) Q[(int64_t)r * ld + (cc - H)] = e[k];
+      }
+    }
+  }
+  struct Pre {};
+  __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&) const {
+    apply4(r, c, v);
+  }
+};
+
+// readout with the x-part precomputed: hn = act((s W_n[:, F:]^T + Q) + b_n)   (GNN.py:106-107)
+struct EpReadoutQ {
+  const float* bias;
+  const float* Q;
+  float* hn;
+  float* zn;  // nullptr for ReLU
+  int64_t ld;
+  int M, N;
+  int act;
+  typedef float4 Pre;
+  __device__ __forceinline__ Pre pre4(int r, int c) const {
+    const bool ok = r < M && c < N;
+    return *reinterpret_cast<const float4*>(Q + (ok ? (int64_t)r * ld + c : 0));
+  }
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& q) const {
+    if (r >= M || c >= N) return;
+    const int64_t o = (int64_t)r * ld + c;
+    float z[4] = {v.x + q.x, v.y + q.y, v.z + q.z, v.w + q.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] += bias[min(c + k, N - 1)];
+    if (zn) *reinterpret_cast<float4*>(zn + o) = make_float4(z[0], z[1], z[2], z[3]);
+    *reinterpret_cast<float4*>(hn + o) =
+        make_float4(act_fwd(z[0], act), act_fwd(z[1], act), act_fwd(z[2], act), act_fwd(z[3], act));
+  }
+  __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
+    if (r >= M || c >= N) return;
+    apply4p(r, c, v, *reinterpret_cast<const float4*>(Q + (int64_t)r * ld + c));
+  }
+};
+
 // edge_to_node readout (GNN.py:106-107): hn = act([x | s] W_n^T + b_n)
 struct EpReadout {
   const float* bias;

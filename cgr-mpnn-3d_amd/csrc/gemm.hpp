@@ -96,6 +96,33 @@ struct LdPlain {
   }
 };
 
+// B rows of two stacked weight matrices: rows [0, n0) from base0 (ld0), rows [n0, ...) from base1
+// (ld1).  Used for the merged x-GEMM  x @ [W0[:, :F]; W_n[:, :F]]^T.  VEC divides ld0, ld1, K.
+template <int VEC>
+struct LdTwoRows {
+  const float* base0;
+  int64_t ld0;
+  const float* base1;
+  int64_t ld1;
+  int n0;
+  struct Row {
+    const float* p;
+    bool ok;
+  };
+  typedef float4 Raw;
+  __device__ __forceinline__ Row row(int r, int limit) const {
+    const bool ok = r < limit;
+    const int rr = ok ? r : 0;
+    return Row{rr < n0 ? base0 + (int64_t)rr * ld0 : base1 + (int64_t)(rr - n0) * ld1, ok};
+  }
+  __device__ __forceinline__ Raw fetch(const Row& rw, int k, int K) const {
+    return fetch4<VEC>(rw.p, k, K);
+  }
+  __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
+    return mask4(v, rw.ok, k, K);
+  }
+};
+
 // m[e, :] = a[src[e], :] - h[rev[e], :]   (GNN.py:136-141).  Internal buffers, ld = Hp (% 4 == 0).
 // REV_XOR: rev[e] = e ^ 1 (caller's original edge order, no index array).  Row keeps the raw
 // indices; addresses are formed in fetch() so the index loads are waited for only there.

@@ -3,8 +3,7 @@
 // forward with src and dst swapped; weight gradients are split-K TN GEMMs over the edge / node
 // dimension reduced deterministically; no atomics anywhere, so gradients are bitwise stable.
 //
-//   dg = dy wf ; dwf = dy^T g ; dbf = sum dy                          (ffn + add-pool)
-//   dzn = dg[graph(v)] * act'(zn)                                     (edge_to_node act)
+//   dwf = dy^T g ; dbf = sum dy ; dzn = dy[graph(v)] wf * act'(zn)        (ffn, pool, edge_to_node)
 //   dW_n = dzn^T [x | s], db_n = colsum(dzn), ds = dzn W_n[:, F:]
 //   dh_D = ds[dst]
 //   for l = D-1 .. 0:
@@ -13,30 +12,40 @@
 //     dm = dpre W_l ; da = segsum_src(dm) ; dh_l = da[dst] - dm[rev]
 //   dpre0 = (dh0 + dh_0) * act'(pre0)
 //   dW0[:, F:] = dpre0^T e ; db0 = colsum(dpre0) ; dW0[:, :F] = (segsum_src dpre0)^T x
+//
+// Streams: the critical path is act_bwd -> dm GEMM -> segsum per layer.  Every weight-gradient
+// TN GEMM (+ its slab reduction) only feeds the gradient outputs, so it runs on the side stream,
+// forked right after its input is produced; dpre is double-buffered so the next layer's act_bwd
+// can proceed, and the main stream waits for the side stream only before re-using a dpre buffer
+// and at the very end.
 #include "dispatch.hpp"
 #include "epilogues.hpp"
 #include "gnn_internal.hpp"
 #include "kernels.hpp"
 #include "profiling.hpp"
+#include "streams.hpp"
 
 namespace cgr {
 
 void dropout_params(const float* dropout_p, int training, int l, uint32_t* thresh, float* scale);
 
 template <class AL, class BL>
-static hipError_t tn_and_reduce(const AL& al, const BL& bl, int Nout, int Kout, int R,
-                                float* slab, float* bslab, float* dst, int64_t ld_dst,
-                                int64_t col_off, float* bias_dst, hipStream_t st) {
-  const TnPlan p = tn_plan(Nout, Kout, R);
-  ProfScope _p1("gemm_tn_wgrad", st);
-  hipError_t e = with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
-    return launch_gemm_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(al, bl, p, slab, bslab, Nout,
-                                                                   Kout, R, bias_dst != nullptr,
-                                                                   st);
+static hipError_t tn_gemm(const AL& al, const BL& bl, int Nout, int Kout, int R, float* slab,
+                          float* bslab, bool want_bias, TnPlan* plan, hipStream_t st) {
+  *plan = tn_plan(Nout, Kout, R);
+  const TnPlan p = *plan;
+  ProfScope _p("gemm_tn_wgrad", st);
+  return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
+    return launch_gemm_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(al, bl, p, slab, bslab,
+                                                                         Nout, Kout, R, want_bias,
+                                                                         st);
   });
-  if (e != hipSuccess) return e;
-  _p1.end();
-  ProfScope _p2("splitk_reduce", st);
+}
+
+static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
+                            int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
+                            hipStream_t st) {
+  ProfScope _p("splitk_reduce", st);
   return reduce_slabs(slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, st);
 }
 
@@ -48,21 +57,28 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   const FloatView fv = float_view(const_cast<void*>(arena), L, d);
   const WorkspaceLayout WL = workspace_layout(d);
   char* ws = static_cast<char*>(workspace);
-  float* dpre = reinterpret_cast<float*>(ws + WL.dpre);
+  float* dpre[2] = {reinterpret_cast<float*>(ws + WL.dpre[0]),
+                    reinterpret_cast<float*>(ws + WL.dpre[1])};
   float* dm = reinterpret_cast<float*>(ws + WL.dm);
   float* dh0 = reinterpret_cast<float*>(ws + WL.dh0);
   float* da = reinterpret_cast<float*>(ws + WL.da);
   float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
   float* ds = reinterpret_cast<float*>(ws + WL.ds);
   float* Gs = reinterpret_cast<float*>(ws + WL.Gs);
-  float* dg = reinterpret_cast<float*>(ws + WL.dg);
   float* wT = reinterpret_cast<float*>(ws + WL.wT);
   float* slab = reinterpret_cast<float*>(ws + WL.slab);
   float* bslab = reinterpret_cast<float*>(ws + WL.bslab);
+  float* slab2 = reinterpret_cast<float*>(ws + WL.slab2);
+  float* bslab2 = reinterpret_cast<float*>(ws + WL.bslab2);
   float* dsig_part = reinterpret_cast<float*>(ws + WL.dsig_part);
 
   const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
   const int64_t HHp = (int64_t)H * Hp;
+
+  SideStreams* ss = side_streams(st);
+  if (!ss) return CGR_ERR_HIP;
+  // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
+  hipStream_t side = prof_enabled() ? st : ss->side;
 
   // transposed weights: wT[l] = W_l^T (l < D), wT[D] = W_n[:, F:]^T, all [H, Hp]
   {
@@ -78,21 +94,26 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // head + readout
   {
     ProfScope _p("head_readout_bwd", st);
-    HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, dg,
+    HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
                      grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], st));
     HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H, Hp,
                             d.act, dzn, st));
   }
+  // side: dW_n = dzn^T [x | s], db_n
+  HIP_RET(fork_to(ss, st, side));
   {
     const int vx = vec_for(b->x, F, F);
+    TnPlan p;
     hipError_t e = with_vec(vx, [&](auto VX) {
       LdPlain<4> al{dzn, Hp};
       LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
-      return tn_and_reduce(al, bl, H, F + H, N, slab, bslab, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
-                           grads[CGR_PARAM_E2N_B(D)], st);
+      return tn_gemm(al, bl, H, F + H, N, slab, bslab, true, &p, side);
     });
     HIP_RET(e);
+    HIP_RET(tn_reduce(p, slab, bslab, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
+                      grads[CGR_PARAM_E2N_B(D)], side));
   }
+  // main: ds = dzn W_n[:, F:]
   {
     ProfScope _p("gemm_nt_bwd", st);
     hipError_t e = with_nt_rn(H, [&](auto RN) {
@@ -104,8 +125,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     HIP_RET(e);
   }
 
-  int nb = layer_act_bwd_blocks(E, Hp);
+  const int nb = layer_act_bwd_blocks(E, Hp);
+  hipEvent_t tn_done[CGR_MAX_DEPTH];
   for (int l = D - 1; l >= 0; --l) {
+    float* dp = dpre[l & 1];
+    if (l + 2 <= D - 1) HIP_RET(hipStreamWaitEvent(st, tn_done[l + 2], 0));  // buffer reuse
     uint32_t thresh;
     float scale;
     dropout_params(dropout_p, training, l, &thresh, &scale);
@@ -128,65 +152,74 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.E = E;
     la.H = H;
     la.Hp = Hp;
-    la.dpre = dpre;
+    la.dpre = dp;
     la.dh0 = dh0;
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
     {
       ProfScope _p("layer_act_bwd", st);
       HIP_RET(layer_act_bwd(la, nullptr, st));
     }
-
-    // dW_l = dpre^T m_l, db_l = colsum(dpre)
+    // side: dW_l = dpre^T m_l, db_l = colsum(dpre)
+    HIP_RET(fork_to(ss, st, side));
     {
-      LdPlain<4> al{dpre, Hp};
+      LdPlain<4> al{dp, Hp};
       LdGatherDiff<false> bl{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
-      HIP_RET(tn_and_reduce(al, bl, H, H, E, slab, bslab, grads[CGR_PARAM_CONV_W(l)], H, 0,
-                            grads[CGR_PARAM_CONV_B(l)], st));
+      TnPlan p;
+      HIP_RET(tn_gemm(al, bl, H, H, E, slab, bslab, true, &p, side));
+      HIP_RET(record_point(ss, side, &tn_done[l]));
+      HIP_RET(tn_reduce(p, slab, bslab, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
+                        grads[CGR_PARAM_CONV_B(l)], side));
     }
-    // dm = dpre W_l
+    // main: dm = dpre W_l ; da[v] = sum_{src(e) = v} dm[e]
     {
       ProfScope _p("gemm_nt_bwd", st);
       hipError_t e = with_nt_rn(H, [&](auto RN) {
-        LdPlain<4> al{dpre, Hp};
+        LdPlain<4> al{dp, Hp};
         LdPlain<4> bl{wT + l * HHp, Hp};
         EpStore ep{dm, Hp, E, H, nullptr};
         return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H, st);
       });
       HIP_RET(e);
     }
-    // da[v] = sum_{src(e) = v} dm[e]
     {
       ProfScope _p("segsum_src_bwd", st);
       HIP_RET(segment_sum(dm, Hp, iv.src_list, iv.src_ptr, N, Hp, da, Hp, st));
     }
   }
 
-  // edge init
+  // edge init: dpre0 overwrites dh0 in place (each element read then written by one thread)
+  float* dpre0 = dh0;
   {
     ProfScope _p("edge_init_bwd", st);
     HIP_RET(edge_init_bwd(dh0, da, dm, iv.dst_s, iv.rev_s, fv.h[0], fv.pre[0], E, H, Hp, d.act,
-                          dpre, st));
+                          dpre0, st));
   }
   float* gW0 = grads[CGR_PARAM_EDGE_INIT_W];
   float* gb0 = grads[CGR_PARAM_EDGE_INIT_B];
-  if (Fe > 0) {
-    LdPlain<4> al{dpre, Hp};
+  if (Fe > 0) {  // side: dW0[:, F:] = dpre0^T e, db0
+    HIP_RET(fork_to(ss, st, side));
+    LdPlain<4> al{dpre0, Hp};
     LdPlain<4> bl{fv.e_s, d.Fep};
-    HIP_RET(tn_and_reduce(al, bl, H, Fe, E, slab, bslab, gW0, F + Fe, F, gb0, st));
+    TnPlan p;
+    HIP_RET(tn_gemm(al, bl, H, Fe, E, slab, bslab, true, &p, side));
+    HIP_RET(tn_reduce(p, slab, bslab, H, Fe, gW0, F + Fe, F, gb0, side));
   }
   {
     ProfScope _p("segsum_src_bwd", st);
-    HIP_RET(segment_sum(dpre, Hp, iv.src_list, iv.src_ptr, N, Hp, Gs, Hp, st));
+    HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, Hp, Gs, Hp, st));
   }
-  {
+  if (F > 0) {  // main: dW0[:, :F] = Gs^T x (own slab: runs beside the side stream's work)
     const int vx = vec_for(b->x, F, F);
+    TnPlan p;
     hipError_t e = with_vec(vx, [&](auto VX) {
       LdPlain<4> al{Gs, Hp};
       LdPlain<decltype(VX)::value> bl{b->x, F};
-      return tn_and_reduce(al, bl, H, F, N, slab, bslab, gW0, F + Fe, 0,
-                           Fe > 0 ? nullptr : gb0, st);
+      return tn_gemm(al, bl, H, F, N, slab2, bslab2, Fe == 0, &p, st);
     });
     HIP_RET(e);
+    HIP_RET(tn_reduce(p, slab2, bslab2, H, F, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st));
+  } else if (Fe == 0) {
+    HIP_RET(hipMemsetAsync(gb0, 0, sizeof(float) * H, st));
   }
 
   if (d.learnable_skip) {
@@ -196,6 +229,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     ProfScope _p("skip_grad_reduce", st);
     HIP_RET(reduce_partials(dsig_part, nb, sj, st));
   }
+  // join: every gradient is complete when the main stream reaches here
+  HIP_RET(depend(ss, side, st));
   return 0;
 }
 

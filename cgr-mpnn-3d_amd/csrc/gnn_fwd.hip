@@ -1,19 +1,22 @@
-// GNN.forward (GNN.py:76-110) as a sequence of HIP launches on one stream.
+// GNN.forward (GNN.py:76-110) as HIP launches on the caller's stream plus one side stream.
 //
-//   prep          graph bookkeeping (graph_prep.hip)
-//   P   = x W0x^T node-level half of edge init: N*F*H instead of E*F*H FLOPs (no [E, F+Fe] cat)
-//   h0  = act(P[src] + e W0e^T + b0)                                      (GNN.py:85-87)
-//   a0  = segsum_dst(h0)                                                  (GNN.py:134)
-//   for l: h_{l+1} = drop(act((a_l[src] - h_l[rev]) W_l^T + b_l + s_l h0))  gather->MFMA->epilogue
-//          a_{l+1} = segsum_dst(h_{l+1})                                  (GNN.py:90-102, 134)
-//   hn  = act([x | a_D] W_n^T + b_n)   (a_D IS the readout aggregate s)   (GNN.py:105-107)
-//   y   = (sum_{v in graph} hn[v]) . wf + bf                               (GNN.py:110)
+//   side:  [P | Q] = x [W0[:, :F]; W_n[:, :F]]^T   one GEMM reads x once; P = node-level half of
+//          edge init (N*F*H instead of E*F*H FLOPs), Q = x-part of the readout; runs while the
+//          main stream does the graph bookkeeping (it needs neither)
+//   main:  graph prep ; join
+//          h0  = act(P[src] + e W0e^T + b0)                                     (GNN.py:85-87)
+//          a0  = segsum_dst(h0)                                                 (GNN.py:134)
+//          for l: h_{l+1} = drop(act((a_l[src] - h_l[rev]) W_l^T + b_l + s_l h0))
+//                 a_{l+1} = segsum_dst(h_{l+1})                            (GNN.py:90-102, 134)
+//          hn  = act(a_D W_n[:, F:]^T + Q + b_n)   (a_D IS the readout aggregate s, GNN.py:105-107)
+//          y   = (sum_{v in graph} hn[v]) . wf + bf                             (GNN.py:110)
 // The reference's discarded readout GEMM (GNN.py:105 -> lin(...) at :141) is not executed.
 #include "dispatch.hpp"
 #include "epilogues.hpp"
 #include "gnn_internal.hpp"
 #include "kernels.hpp"
 #include "profiling.hpp"
+#include "streams.hpp"
 
 namespace cgr {
 
@@ -49,40 +52,55 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
   const float* W0 = params[CGR_PARAM_EDGE_INIT_W];
   const float* b0 = params[CGR_PARAM_EDGE_INIT_B];
+  const float* Wn = params[CGR_PARAM_E2N_W(D)];
+  const float* bn = params[CGR_PARAM_E2N_B(D)];
 
-  PrepArgs pa{b->edge_index, b->batch, b->graph_ptr, b->edge_attr, d.N, d.E, d.B,
-              d.Fe,          d.Fep,   iv,           fv.e_s};
-  {
-    ProfScope _p("graph_prep", st);
-    int rc = cgr_graph_prep_impl(pa, st);
-    if (rc) return rc;
-  }
+  SideStreams* ss = side_streams(st);
+  if (!ss) return CGR_ERR_HIP;
+  // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
+  hipStream_t side = prof_enabled() ? st : ss->side;
+  HIP_RET(fork_to(ss, st, side));
 
-  // edge-feature slice of edge_init.weight, transposed to [Fe, Hp]
+  // ---- side stream: edge-feature weight slice + merged x-GEMM ----
   if (Fe > 0) {
-    ProfScope _p("weight_transpose", st);
+    ProfScope _p("weight_transpose", side);
     TransposeJobs tj{};
     tj.job[0] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
     tj.n = 1;
-    HIP_RET(transpose_batch(tj, st));
+    HIP_RET(transpose_batch(tj, side));
   }
-
-  // P = x @ W0[:, :F]^T   [N, Hp]
-  {
-    ProfScope _p("gemm_nt_node_P", st);
-    const int vx = vec_for(b->x, F, F), vw = vec_for(W0, F + Fe, F);
+  if (F > 0) {
+    ProfScope _p("gemm_nt_x", side);
+    int vb = vec_for(W0, F + Fe, F);
+    const int vb2 = vec_for(Wn, F + H, F);
+    vb = vb < vb2 ? vb : vb2;
+    const int vx = vec_for(b->x, F, F);
     hipError_t e = with_vec(vx, [&](auto VX) {
-      return with_vec(vw, [&](auto VW) {
-        return with_nt_rn(H, [&](auto RN) {
+      return with_vec(vb, [&](auto VB) {
+        return with_nt_rn(2 * H, [&](auto RN) {
           LdPlain<decltype(VX)::value> al{b->x, F};
-          LdPlain<decltype(VW)::value> bl{W0, F + Fe};
-          EpStore ep{fv.P, Hp, N, H, nullptr};
-          return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, H, F, st);
+          LdTwoRows<decltype(VB)::value> bl{W0, F + Fe, Wn, F + H, H};
+          EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
+          return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, 2 * H, F, side);
         });
       });
     });
     HIP_RET(e);
+  } else {
+    HIP_RET(hipMemsetAsync(fv.P, 0, sizeof(float) * (size_t)N * Hp, side));
+    HIP_RET(hipMemsetAsync(fv.Q, 0, sizeof(float) * (size_t)N * Hp, side));
   }
+
+  // ---- main stream: graph bookkeeping, then join ----
+  {
+    ProfScope _p("graph_prep", st);
+    PrepArgs pa{b->edge_index, b->batch, b->graph_ptr, b->edge_attr, d.N, d.E, d.B,
+                d.Fe,          d.Fep,   iv,           fv.e_s};
+    int rc = cgr_graph_prep_impl(pa, st);
+    if (rc) return rc;
+  }
+  HIP_RET(depend(ss, side, st));
+
   {
     ProfScope _p("edge_init_fwd", st);
     HIP_RET(edge_init_fwd(fv.P, iv.src_s, fv.e_s, Fe, d.Fep, fv.w0eT, b0, E, H, Hp, d.act,
@@ -107,34 +125,31 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
                scale,    seed,
                l};
     LdGatherDiff<false> al{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
-    const int vw = vec_for(Wl, H, H);
-    ProfScope _p1("gemm_nt_layer_fwd", st);
-    hipError_t e = with_vec(vw, [&](auto VW) {
-      return with_nt_rn(H, [&](auto RN) {
-        LdPlain<decltype(VW)::value> blw{Wl, H};
-        return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, E, H, H, st);
+    {
+      ProfScope _p("gemm_nt_layer_fwd", st);
+      const int vw = vec_for(Wl, H, H);
+      hipError_t e = with_vec(vw, [&](auto VW) {
+        return with_nt_rn(H, [&](auto RN) {
+          LdPlain<decltype(VW)::value> blw{Wl, H};
+          return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, E, H, H, st);
+        });
       });
-    });
-    HIP_RET(e);
-    _p1.end();
+      HIP_RET(e);
+    }
     ProfScope _p2("segsum_dst_fwd", st);
     HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
   }
 
-  // readout: hn = act([x | s] W_n^T + b_n), s = a_D
+  // readout: hn = act(s W_n[:, F:]^T + Q + b_n), s = a_D
   {
     ProfScope _p("gemm_nt_readout_fwd", st);
-    const float* Wn = params[CGR_PARAM_E2N_W(D)];
-    const float* bn = params[CGR_PARAM_E2N_B(D)];
-    const int vx = vec_for(b->x, F, F), vw = vec_for(Wn, F + H, F + H);
-    EpReadout ep{bn, fv.hn, fv.zn, Hp, N, H, d.act};
-    hipError_t e = with_vec(vx, [&](auto VX) {
-      return with_vec(vw, [&](auto VW) {
-        return with_nt_rn(H, [&](auto RN) {
-          LdConcat<decltype(VX)::value> al{b->x, F, fv.a[D], Hp, F};
-          LdPlain<decltype(VW)::value> blw{Wn, F + H};
-          return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, blw, ep, N, H, F + H, st);
-        });
+    const int vw = vec_for(Wn + F, F + H, H);
+    EpReadoutQ ep{bn, fv.Q, fv.hn, fv.zn, Hp, N, H, d.act};
+    hipError_t e = with_vec(vw, [&](auto VW) {
+      return with_nt_rn(H, [&](auto RN) {
+        LdPlain<4> al{fv.a[D], Hp};
+        LdPlain<decltype(VW)::value> blw{Wn + F, F + H};
+        return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, N, H, H, st);
       });
     });
     HIP_RET(e);

@@ -1,0 +1,64 @@
+#include "streams.hpp"
+
+#include <mutex>
+#include <string>
+
+#include "gnn_internal.hpp"
+
+namespace cgr {
+
+namespace {
+std::mutex g_mu;
+SideStreams* g_side[64] = {nullptr};
+}  // namespace
+
+SideStreams* side_streams(hipStream_t main) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+    set_error("cgr: hipGetDevice failed");
+    return nullptr;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_side[dev]) return g_side[dev];
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (main && hipStreamIsCapturing(main, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    set_error("cgr: first native call on this device happened inside a stream capture; run one "
+              "eager step before capturing (side streams/events are created lazily)");
+    return nullptr;
+  }
+  SideStreams* s = new SideStreams();
+  if (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess) {
+    set_error("cgr: hipStreamCreate failed");
+    delete s;
+    return nullptr;
+  }
+  for (auto& e : s->ev) {
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      set_error("cgr: hipEventCreate failed");
+      return nullptr;
+    }
+  }
+  s->next = 0;
+  g_side[dev] = s;
+  return s;
+}
+
+hipError_t depend(SideStreams* s, hipStream_t from, hipStream_t to) {
+  hipEvent_t e = s->ev[s->next];
+  s->next = (s->next + 1) % 16;
+  hipError_t r = hipEventRecord(e, from);
+  if (r != hipSuccess) return r;
+  return hipStreamWaitEvent(to, e, 0);
+}
+
+hipError_t record_point(SideStreams* s, hipStream_t from, hipEvent_t* ev) {
+  *ev = s->ev[s->next];
+  s->next = (s->next + 1) % 16;
+  return hipEventRecord(*ev, from);
+}
+
+hipError_t fork_to(SideStreams* s, hipStream_t main, hipStream_t side) {
+  return depend(s, main, side);
+}
+
+}  // namespace cgr

@@ -1,0 +1,28 @@
+// Side streams for off-critical-path work (weight-gradient GEMMs, the x-GEMM beside graph prep).
+// fork(main -> side) / join(side -> main) with events; under stream capture both become graph
+// edges, so a captured step keeps the concurrency.  Streams and events are created once per device
+// (lazily, on the first call, which must not be inside a capture: the library's own warm-up
+// happens eagerly in every caller we ship; a first call inside a capture returns an error).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace cgr {
+
+struct SideStreams {
+  hipStream_t side;
+  hipEvent_t ev[16];
+  int next;
+};
+
+// returns nullptr and sets the library error if the streams cannot be created
+SideStreams* side_streams(hipStream_t main);
+
+// main -> side dependency (side waits for everything enqueued on main so far)
+hipError_t fork_to(SideStreams* s, hipStream_t main, hipStream_t side);
+// record a point on `from` and make `to` wait for it
+hipError_t depend(SideStreams* s, hipStream_t from, hipStream_t to);
+// record a point on `from` for a later wait (the ring holds 16 events: wait within 16 records)
+hipError_t record_point(SideStreams* s, hipStream_t from, hipEvent_t* ev);
+
+}  // namespace cgr

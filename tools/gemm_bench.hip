@@ -13,6 +13,7 @@
 
 #include "../cgr-mpnn-3d_amd/csrc/epilogues.hpp"
 #include "../cgr-mpnn-3d_amd/csrc/gemm.hpp"
+#include "../cgr-mpnn-3d_amd/csrc/gemm_ws.hpp"
 
 using namespace cgr;
 
@@ -92,12 +93,28 @@ int main(int argc, char** argv) {
     if (!ref_nt) ref_nt = o;                                                                      \
   }
   NTV(4, 1, 5, 1)
-  NTV(4, 1, 5, 2)
-  NTV(4, 2, 5, 1)
-  NTV(4, 2, 5, 2)
-  NTV(8, 1, 5, 1)
-  NTV(8, 1, 5, 2)
-  NTV(2, 1, 5, 2)
+  int ncu = 256;
+  {
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    ncu = prop.multiProcessorCount;
+  }
+#define WSV(RN_, P_, GRP_SCALE)                                                                  \
+  {                                                                                               \
+    float* o = out_buf((size_t)E * Hp);                                                           \
+    EpLayer ep{bias, nullptr, h0, o, nullptr, Hp, E, H, ACT_RELU, 0u, 1.f, 0, 0};                 \
+    WsPlan p = plan_ws<RN_, P_>(E, H, H, ncu * GRP_SCALE);                                        \
+    vs.push_back({"ws<" #RN_ "," #P_ "> x" #GRP_SCALE, fl_layer,                                 \
+                  [=](hipStream_t s) {                                                            \
+                    (void)launch_gemm_ws<RN_, P_>(gd, W, H, ep, E, H, H, p, s);                   \
+                  },                                                                              \
+                  o, (size_t)E * Hp, ref_nt});                                                    \
+  }
+  WSV(5, 5, 1)
+  WSV(5, 1, 1)
+  WSV(5, 3, 1)
+  WSV(4, 4, 1)
+  WSV(5, 5, 2)
   // ---- TN layer weight gradient (dpre^T m) ----
   float* dpre = dev_rand((size_t)E * Hp, 11);
   LdPlain<4> ad{dpre, Hp};
