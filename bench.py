@@ -7,7 +7,8 @@
 A step is one pass of the hot path over one synthetic, HBM-resident batch of BASELINE config 2
 (256 reactions per GPU, 30 atoms / 60 directed edges each, F = 846, Fe = 14, depth 4, hidden
 400): forward, MSELoss(sum), backward (native), RCCL all-reduce(SUM) of the flat gradient
-bucket when N > 1, Adam(amsgrad) step (train.py:117-121).  Per-GPU work is fixed (weak scaling).
+bucket when N > 1, Adam(amsgrad) step (train.py:117-121; the fused native FusedAdam by default,
+--optimizer torch for torch.optim.Adam).  Per-GPU work is fixed (weak scaling).
 Rank 0 prints ONE JSON line.  See DESIGN.md "Measurement".
 """
 
@@ -43,6 +44,10 @@ def parse():
     ap.add_argument("--config", default="cfg2", choices=["cfg1", "cfg2", "cfg4", "cfg5"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a HIP graph (1/0; -1 = auto: on for N = 1)")
+    ap.add_argument("--optimizer", default="fused", choices=["fused", "torch"],
+                    help="fused: cgr FusedAdam (one native launch); torch: torch.optim.Adam")
+    ap.add_argument("--dropout", type=float, default=0.02,
+                    help="dropout p per layer (train.py default 0.02)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=10,
@@ -52,30 +57,42 @@ def parse():
 
 
 # ------------------------------------------------------------------------------------------------
-# algorithmic work per kernel class and step (DESIGN.md "Roofline accounting")
+# algorithmic work per LAUNCH of each kernel class (DESIGN.md "Roofline accounting").  Bytes count
+# each operand once (gathered rows of an N-row table count as the table), fp32 = 4 B, int32 index
+# = 4 B; flops = 2 per multiply-add.  Classes match the native ProfScope names; every launch of a
+# class has the same shape, so (per-launch work) / (average launch time) is the achieved rate.
 # ------------------------------------------------------------------------------------------------
 def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
-    f4 = 4
-    pre = 0 if relu else 1
+    f4, i4 = 4.0, 4.0
+    pre = 0 if relu else 1       # ReLU's derivative is read off the output; others keep pre-act
     w = {}
-    w["gemm_nt_layer_fwd"] = dict(
-        flops=D * 2.0 * E * H * H,
-        bytes=D * f4 * (N * H + E * H + E * H + E * H * (1 + pre) + H * H) + D * 8.0 * E)
-    w["gemm_nt_node_P"] = dict(flops=2.0 * N * F * H, bytes=f4 * (N * F + H * F + N * H))
-    w["gemm_nt_readout_fwd"] = dict(flops=2.0 * N * (F + H) * H,
-                                    bytes=f4 * (N * F + N * H + H * (F + H) + N * H * (1 + pre)))
-    w["gemm_nt_bwd"] = dict(flops=D * 2.0 * E * H * H + 2.0 * N * H * H,
-                            bytes=f4 * (D * (2 * E * H + H * H) + 2 * N * H + H * H))
-    tn_flops = 2.0 * N * H * (F + H) + D * 2.0 * E * H * H + 2.0 * E * H * Fe + 2.0 * N * H * F
-    tn_bytes = f4 * (N * H + N * (F + H) + D * (E * H + N * H + E * H) + E * H + E * Fe
-                     + N * H + N * F)
-    w["gemm_tn_wgrad"] = dict(flops=tn_flops, bytes=tn_bytes)
-    # scatter-add (segmented sum over dst CSR): read E rows, write N rows, + indices
-    seg = f4 * (E * H + N * H) + 4.0 * (N + 1)
-    w["segsum_dst_fwd"] = dict(flops=float((D + 1) * E * H), bytes=(D + 1) * seg)
-    w["segsum_src_bwd"] = dict(flops=float((D + 1) * E * H),
-                               bytes=(D + 1) * (seg + 4.0 * E))
-    w["layer_act_bwd"] = dict(flops=0.0, bytes=D * f4 * (E * H * 5 + N * H))
+
+    def add(name, launches, flops, nbytes):
+        w[name] = dict(launches=launches, flops=float(flops), bytes=float(nbytes))
+
+    # forward
+    add("gemm_nt_x", 1, 2.0 * N * F * 2 * H, f4 * (N * F + 2 * H * F + 2 * N * H))
+    add("edge_init_fwd", 1, 2.0 * E * Fe * H,
+        f4 * (N * H + E * Fe + Fe * H + H + E * H * (1 + pre)) + i4 * E)
+    seg_dst = f4 * (E * H + N * H) + i4 * (N + 1)
+    add("segsum_dst_fwd", D + 1, E * H, seg_dst)
+    add("gemm_nt_layer_fwd", D, 2.0 * E * H * H,
+        f4 * (N * H + E * H + E * H + H * H + H + E * H * (1 + pre)) + 2 * i4 * E)
+    add("gemm_nt_readout_fwd", 1, 2.0 * N * H * H, f4 * (N * H + N * H + H * H + H + 2 * N * H))
+    add("pool_head_fwd", 1, 2.0 * N * H, f4 * (N * H + B * H + H + B) + i4 * (B + 1))
+    # backward
+    add("head_readout_bwd", 1, 2.0 * N * H, f4 * (B + 2 * N * H + B * H + 2 * H + N * H))
+    add("gemm_tn_wgrad_readout", 1, 2.0 * N * H * (F + H),
+        f4 * (N * H + N * F + N * H + H * (F + H) + H))
+    add("gemm_nt_readout_bwd", 1, 2.0 * N * H * H, f4 * (N * H + H * H + N * H))
+    add("layer_act_bwd", D, 0.0, f4 * (N * H + 5 * E * H) + 2 * i4 * E)
+    add("gemm_tn_wgrad_layer", D, 2.0 * E * H * H,
+        f4 * (E * H + N * H + E * H + H * H + H) + 2 * i4 * E)
+    add("gemm_nt_layer_bwd", D, 2.0 * E * H * H, f4 * (E * H + H * H + E * H))
+    add("segsum_src_bwd", D + 1, E * H, seg_dst + i4 * E)
+    add("edge_init_bwd", 1, 0.0, f4 * (N * H + 4 * E * H) + 2 * i4 * E)
+    add("gemm_tn_wgrad_edge", 1, 2.0 * E * H * Fe, f4 * (E * H + E * Fe + H * Fe + H))
+    add("gemm_tn_wgrad_node", 1, 2.0 * N * H * F, f4 * (N * H + N * F + H * F))
     return w
 
 
@@ -83,24 +100,25 @@ def mfma_bound(name):
     return name.startswith("gemm")
 
 
-def roofline_entry(name, work, ms_per_step, traffic):
-    t = ms_per_step * 1e-3
+def roofline_entry(name, work, launches, ms_total, traffic):
+    """Per-launch roofline: algorithmic work of one launch / average launch duration."""
+    t = ms_total * 1e-3 / launches
     if mfma_bound(name):
         ach = work["flops"] / t / 1e12
-        peak = FP32_MFMA_PEAK_TFLOPS
-        unit = "TFLOP/s"
+        peak, unit = FP32_MFMA_PEAK_TFLOPS, "TFLOP/s"
     else:
         ach = work["bytes"] / t / 1e9
-        peak = HBM_PEAK_GBS
-        unit = "GB/s"
+        peak, unit = HBM_PEAK_GBS, "GB/s"
     return {"kernel": name, "bound": "mfma" if mfma_bound(name) else "hbm",
             "achieved": round(ach, 3), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-            "traffic": traffic, "algorithmic_bytes": work["bytes"],
-            "algorithmic_flops": work["flops"], "ms_per_step": round(ms_per_step, 5)}
+            "traffic": traffic, "algorithmic_bytes_per_launch": work["bytes"],
+            "algorithmic_flops_per_launch": work["flops"],
+            "avg_launch_us": round(t * 1e6, 3), "launches_measured": launches,
+            "timing": "HIP events on the launch stream, instrumented serial pass"}
 
 
 # ------------------------------------------------------------------------------------------------
-def cpu_baseline(cfgname, seconds):
+def cpu_baseline(cfgname, seconds, dropout):
     """Reference CPU path (oracle/dmpnn_torch.py: the reference ATen op sequence incl. its dead
     readout GEMM) on this host's cores: same batch shape, MSE(sum) + backward + Adam(amsgrad)."""
     from cgr_mpnn_3D._amd.synth import CONFIGS, make_batch
@@ -110,7 +128,8 @@ def cpu_baseline(cfgname, seconds):
     b = make_batch(c["num_graphs"], c["n_atoms"], c["n_bonds"], c["n_mace"], seed=1234)
     F_ = b.x.shape[1]
     sd = random_state_dict(F_, 14, c["hidden"], c["depth"], c["learnable_skip"], seed=0)
-    m = TorchRestatement(sd, c["depth"], learnable_skip=c["learnable_skip"])
+    m = TorchRestatement(sd, c["depth"], learnable_skip=c["learnable_skip"],
+                         dropout_ps=[dropout] * c["depth"])
     m.train()
     opt = torch.optim.Adam(m.parameters(), lr=1e-3, amsgrad=True)
     x = torch.from_numpy(b.x)
@@ -171,12 +190,18 @@ def main():
     N, E, B = b.x.shape[0], b.edge_index.shape[1], b.num_graphs
     F_ = b.x.shape[1]
     torch.manual_seed(0)
-    model = GNN(F_, 14, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D,
+    model = GNN(F_, 14, depth=D, hidden_sizes=[H] * D, dropout_ps=[args.dropout] * D,
                 use_learnable_skip=c["learnable_skip"]).to(dev)
     model.train()
     if world > 1:
         install_grad_allreduce(model)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-3, amsgrad=True, capturable=bool(args.graph))
+    if args.optimizer == "fused":
+        from cgr_mpnn_3D._amd.optim import FusedAdam
+
+        opt = FusedAdam(model.parameters(), lr=1e-3, amsgrad=True)
+    else:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3, amsgrad=True,
+                               capturable=bool(args.graph))
     loss_fn = torch.nn.MSELoss(reduction="sum")
 
     def step():
@@ -230,6 +255,7 @@ def main():
     lib = native.load()
     roof = None
     roof_scatter = None
+    roof_all = {}
     breakdown = {}
     if args.profile_steps > 0:
         lib.cgr_profile_reset()
@@ -246,23 +272,29 @@ def main():
                 traffic = json.load(open(args.traffic_json)).get(args.config, {})
             except Exception:  # noqa: BLE001
                 traffic = {}
+
+        def hbm(name):
+            t = traffic.get(name)
+            return None if t is None else t.get("hbm_bytes_per_launch")
+
         for name, (cnt, tot) in rep.items():
             breakdown[name] = {"launches_per_step": cnt / args.profile_steps,
                                "ms_per_step": round(tot / args.profile_steps, 5)}
         cands = [k for k in rep if k in work]
         if cands:
             dom = max(cands, key=lambda k: rep[k][1])
-            roof = roofline_entry(dom, work[dom], rep[dom][1] / args.profile_steps,
-                                  traffic.get(dom))
+            roof = roofline_entry(dom, work[dom], rep[dom][0], rep[dom][1], hbm(dom))
         if "segsum_dst_fwd" in rep:
             roof_scatter = roofline_entry("segsum_dst_fwd", work["segsum_dst_fwd"],
-                                          rep["segsum_dst_fwd"][1] / args.profile_steps,
-                                          traffic.get("segsum_dst_fwd"))
+                                          rep["segsum_dst_fwd"][0], rep["segsum_dst_fwd"][1],
+                                          hbm("segsum_dst_fwd"))
+        roof_all = {k: roofline_entry(k, work[k], rep[k][0], rep[k][1], hbm(k))["frac"]
+                    for k in cands}
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         log("[bench] timing the CPU baseline (reference op sequence, torch CPU) ...")
-        cpu = cpu_baseline(args.config, args.cpu_seconds)
+        cpu = cpu_baseline(args.config, args.cpu_seconds, args.dropout)
 
     if rank == 0:
         out = {
@@ -274,11 +306,13 @@ def main():
             "config": {
                 "workload": f"{args.config}: CGR-MPNN-3D depth={D} hidden={H}, {B} reactions/GPU "
                             f"({c['n_atoms']} atoms, {2 * c['n_bonds']} directed edges each), "
-                            f"F={F_} (78 CGR + {c['n_mace']} MACE), Fe=14, ReLU, dropout 0; step "
+                            f"F={F_} (78 CGR + {c['n_mace']} MACE), Fe=14, ReLU, dropout {args.dropout}; step "
                             f"= fwd + MSELoss(sum) + bwd + grad all-reduce (N>1) + "
-                            f"Adam(amsgrad)" + (", HIP-graph captured" if args.graph else ""),
+                            f"Adam(amsgrad, {'fused native' if args.optimizer == 'fused' else 'torch foreach'})"
+                            + (", HIP-graph captured" if args.graph else ""),
                 "global_batch": world * B, "parallelism": f"dp{world}"},
-            "roofline": roof, "roofline_scatter_add": roof_scatter, "kernel_breakdown": breakdown,
+            "roofline": roof, "roofline_scatter_add": roof_scatter,
+            "roofline_frac_by_class": roof_all, "kernel_breakdown": breakdown,
             "cpu_baseline": cpu,
         }
         if cpu:

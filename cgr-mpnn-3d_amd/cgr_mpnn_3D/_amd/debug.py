@@ -28,7 +28,7 @@ class ArenaRun:
         self.dropout_ps, self.seed, self.training = dropout_ps, seed, training
         native.check(lib.cgr_gnn_forward(
             ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
-            _dropout_array(dropout_ps, self.cfg.depth), ctypes.c_uint64(seed), int(training),
+            _dropout_array(dropout_ps, self.cfg.depth), ctypes.c_uint64(seed), None, int(training),
             native.ptr(self.arena), native.ptr(self.y), native.stream_ptr(dev)))
 
     def offset(self, name, index=0):

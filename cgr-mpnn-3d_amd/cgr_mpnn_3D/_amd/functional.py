@@ -58,7 +58,7 @@ class GNNFunction(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs,
-                dropout_ps, seed, training, bucket_hook, *params):
+                dropout_ps, seed, rng_counter, training, bucket_hook, *params):
         lib = native.load()
         cfg = make_config(*cfg_tuple)
         N, E, B = int(x.shape[0]), int(edge_index.shape[1]), int(num_graphs)
@@ -72,8 +72,9 @@ class GNNFunction(torch.autograd.Function):
         ptab = _param_table(params)
         dps = _dropout_array(dropout_ps, cfg.depth)
         native.check(lib.cgr_gnn_forward(ctypes.byref(cfg), ptab, ctypes.byref(bs), dps,
-                                         ctypes.c_uint64(seed), int(bool(training)), native.ptr(arena),
-                                         native.ptr(y), native.stream_ptr(dev)))
+                                         ctypes.c_uint64(seed), native.ptr(rng_counter),
+                                         int(bool(training)), native.ptr(arena), native.ptr(y),
+                                         native.stream_ptr(dev)))
         if _config.strict:
             st = read_status(arena, cfg, N, E, B)
             if st & 1:
@@ -116,10 +117,11 @@ class GNNFunction(torch.autograd.Function):
         hook = ctx.bucket_hook if ctx.bucket_hook is not None else _config.grad_bucket_hook
         if hook is not None:
             hook(flat)  # e.g. RCCL all-reduce of the whole bucket (cgr_mpnn_3D._amd.ddp)
-        return (None,) * 11 + tuple(grads)
+        return (None,) * 12 + tuple(grads)
 
 
 def gnn_forward(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, dropout_ps,
-                seed, training, params, bucket_hook=None):
+                seed, training, params, bucket_hook=None, rng_counter=None):
+    """rng_counter: optional device int64 tensor [1] the forward advances (graph-safe dropout)."""
     return GNNFunction.apply(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs,
-                             dropout_ps, seed, training, bucket_hook, *params)
+                             dropout_ps, seed, rng_counter, training, bucket_hook, *params)

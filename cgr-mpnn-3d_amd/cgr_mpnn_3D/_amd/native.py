@@ -9,13 +9,13 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_float, c_int32, c_int64, c_uint64, c_void_p
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int32, c_int64, c_uint64, c_void_p
 
 _LIB_NAME = "libcgr_mpnn3d.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CGR_MPNN3D_LIB", os.path.join(_HERE, "lib", _LIB_NAME))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_DEPTH = 32
 ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
 
@@ -44,6 +44,21 @@ class CgrBatch(ctypes.Structure):
     ]
 
 
+ADAM_GROUP = 32
+
+
+class CgrAdamTensor(ctypes.Structure):
+    _fields_ = [
+        ("param", c_void_p),
+        ("grad", c_void_p),
+        ("exp_avg", c_void_p),
+        ("exp_avg_sq", c_void_p),
+        ("max_exp_avg_sq", c_void_p),
+        ("step", c_void_p),
+        ("numel", c_int64),
+    ]
+
+
 # (name, restype, argtypes) of every symbol in include/cgr_mpnn3d.h
 SIGNATURES = [
     ("cgr_abi_version", c_int32, []),
@@ -56,7 +71,7 @@ SIGNATURES = [
     ("cgr_graph_prep", c_int32, [POINTER(CgrGnnConfig), POINTER(CgrBatch), c_void_p, c_void_p]),
     ("cgr_gnn_forward", c_int32,
      [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
-      c_int32, c_void_p, c_void_p, c_void_p]),
+      c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     ("cgr_gnn_backward", c_int32,
      [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
       c_int32, c_void_p, c_void_p, POINTER(c_void_p), c_void_p, c_void_p]),
@@ -69,6 +84,9 @@ SIGNATURES = [
     ("cgr_dmpnn_conv_backward", c_int32,
      [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
       c_void_p, c_void_p, c_void_p, c_void_p]),
+    ("cgr_adam_step", c_int32,
+     [POINTER(CgrAdamTensor), c_int32, c_double, c_double, c_double, c_double, c_double, c_int32,
+      c_int32, c_void_p]),
     ("cgr_profile_enable", c_int32, [c_int32]),
     ("cgr_profile_collect", c_int32, []),
     ("cgr_profile_reset", None, []),

@@ -89,6 +89,11 @@ class GNN(nn.Module):
                 nn.Parameter(torch.tensor(1.0)) for _ in range(self.depth))
         # gradient-bucket hook (RCCL all-reduce), set by cgr_mpnn_3D._amd.ddp
         self._grad_bucket_hook = None
+        # device dropout counter: the native forward advances it, so a HIP-graph-captured
+        # training step draws a fresh dropout mask per replay (non-persistent: state_dict keys
+        # stay the reference's)
+        self.register_buffer("_cgr_rng_counter", torch.zeros(1, dtype=torch.int64),
+                             persistent=False)
 
     # -- helpers -------------------------------------------------------------------------------
     def native_parameters(self):
@@ -169,9 +174,13 @@ class GNN(nn.Module):
                 raise RuntimeError("cgr_mpnn_3D (MI355X): parameters must be fp32 CUDA tensors")
         training = self.training and any(p > 0 for p in drop)
         seed = int(torch.randint(0, 2**62, (1,)).item()) if training else 0
+        counter = self._cgr_rng_counter
+        if counter.device != dev:
+            counter = self._cgr_rng_counter = counter.to(dev)
         return gnn_forward((F_, Fe, H, self.depth, act, self.use_learnable_skip), x, edge_index,
                            edge_attr, batch, graph_ptr, num_graphs, drop, seed, training,
-                           [p.contiguous() for p in params], self._grad_bucket_hook)
+                           [p.contiguous() for p in params], self._grad_bucket_hook,
+                           rng_counter=counter)
 
 
 class DMPNNConv(nn.Module):

@@ -14,8 +14,8 @@ static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
 int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
-                     const float* dropout_p, uint64_t seed, int training, void* arena, float* y,
-                     hipStream_t st);
+                     const float* dropout_p, uint64_t seed, uint64_t* rng_counter, int training,
+                     void* arena, float* y, hipStream_t st);
 int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
                       const float* dropout_p, uint64_t seed, int training, const void* arena,
                       const float* dy, float* const* grads, void* workspace, hipStream_t st);
@@ -63,6 +63,7 @@ ArenaLayout arena_layout(const Dims& d) {
   L.status = L.graph_cnt + 4 * B;
   L.zero_bytes = (size_t)round_up((int64_t)(4 * (4 * N + B) + 16), 16);
   b.take(L.zero_bytes);
+  L.rng = b.take(8);
   L.perm = b.take(4 * E);
   L.src_s = b.take(4 * E);
   L.dst_s = b.take(4 * E);
@@ -104,6 +105,7 @@ IndexView index_view(void* arena, const ArenaLayout& L) {
   v.cursor2 = (int*)at(arena, L.cursor2);
   v.graph_cnt = (int*)at(arena, L.graph_cnt);
   v.status = (int*)at(arena, L.status);
+  v.rng = (uint64_t*)at(arena, L.rng);
   v.zero_block = at(arena, L.zero_block);
   v.zero_bytes = L.zero_bytes;
   v.perm = (int*)at(arena, L.perm);
@@ -156,7 +158,8 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   size_t slab = 0, bslab = 0;
   auto acc = [&](int Nout, int Kout, int64_t R) {
     const TnPlan p = tn_plan(Nout, Kout, (int)R);
-    const size_t s = (size_t)p.splits * Nout * Kout, bs = (size_t)p.splits * Nout;
+    const size_t s = (size_t)p.splits * Nout * (size_t)((Kout + 3) & ~3);  // rows padded to 4
+    const size_t bs = (size_t)p.splits * Nout;
     slab = s > slab ? s : slab;
     bslab = bs > bslab ? bs : bslab;
   };
@@ -239,6 +242,7 @@ int64_t cgr_gnn_arena_offset(const cgr_gnn_config* cfg, int64_t N, int64_t E, in
   const std::string n(name);
   const bool li = index >= 0 && index <= CGR_MAX_DEPTH;
   if (n == "status") o = L.status;
+  if (n == "rng") o = L.rng;
   else if (n == "perm") o = L.perm;
   else if (n == "src_s") o = L.src_s;
   else if (n == "dst_s") o = L.dst_s;
@@ -275,8 +279,8 @@ int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* b, void* arena, v
 }
 
 int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,
-                    const float* dropout_p, uint64_t seed, int32_t training, void* arena, float* y,
-                    void* stream) {
+                    const float* dropout_p, uint64_t seed, uint64_t* rng_counter,
+                    int32_t training, void* arena, float* y, void* stream) {
   int rc = validate_config(cfg);
   if (rc) return rc;
   rc = validate_batch(cfg, b);
@@ -286,7 +290,8 @@ int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params, const
   const int np = cgr_gnn_num_params(cfg);
   for (int i = 0; i < np; ++i) CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
   const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
-  return gnn_forward_impl(d, params, b, dropout_p, seed, training, arena, y, (hipStream_t)stream);
+  return gnn_forward_impl(d, params, b, dropout_p, seed, rng_counter, training, arena, y,
+                          (hipStream_t)stream);
 }
 
 int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,

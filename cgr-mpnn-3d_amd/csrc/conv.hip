@@ -46,7 +46,7 @@ ConvLayout conv_layout(int64_t N, int64_t E, int64_t H) {
   L.da = take(4 * N * Hp);
   L.wT = take(4 * H * Hp);
   const TnPlan p = tn_plan((int)H, (int)H, (int)E);
-  L.slab = take(4 * (size_t)p.splits * H * H);
+  L.slab = take(4 * (size_t)p.splits * H * (size_t)((H + 3) & ~3));  // slab rows padded to 4
   L.bslab = take(4 * (size_t)p.splits * H);
   L.bytes = off;
   return L;

@@ -53,7 +53,7 @@ struct EpLayer {
   int act;
   uint32_t thresh;  // dropout: keep iff hash >= thresh (0 = no dropout)
   float scale;      // 1 / (1 - p)
-  uint64_t seed;
+  const uint64_t* seed;  // device: the forward's dropout key (arena "rng"); read iff thresh
   int layer;
   __device__ __forceinline__ void operator()(int r, int c, float v) const {
     if (r >= M || c >= N) return;
@@ -62,7 +62,8 @@ struct EpLayer {
     const float z = (v + bias[c]) + sg * h0[o];
     if (pre) pre[o] = z;
     float h = act_fwd(z, act);
-    if (thresh) h = drop_keep(seed, (uint32_t)layer, (uint64_t)r * N + c, thresh) ? h * scale : 0.f;
+    if (thresh) h = drop_keep(*seed, (uint32_t)layer, (uint64_t)r * N + c, thresh) ? h * scale : 0.f;
+
     else h *= scale;
     hout[o] = h;
   }
@@ -88,11 +89,12 @@ struct EpLayer {
     for (int k = 0; k < 4; ++k) z[k] = (z[k] + bias[min(c + k, N - 1)]) + sg * h0v[k];
     if (pre) *reinterpret_cast<float4*>(pre + o) = make_float4(z[0], z[1], z[2], z[3]);
     float h[4];
+    const uint64_t key = thresh ? *seed : 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       h[k] = act_fwd(z[k], act);
       if (thresh)
-        h[k] = drop_keep(seed, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
+        h[k] = drop_keep(key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
                                                                                  : 0.f;
       else
         h[k] *= scale;

@@ -8,7 +8,7 @@
 //             ([out, in] = nn.Linear layout); an *epilogue* functor consumes C as float4 row
 //             pieces (bias / skip / activation / dropout / stores).
 //   gemm_tn:  C[n, k] = sum_e A(e, n) * B(e, k)      weight gradients dW = dZ^T Q, reduction over
-//             the (long) edge / node dimension, split over gridDim.y into fp32 partial slabs
+//             the (long) edge / node dimension, split into row ranges with fp32 partial slabs
 //             (deterministic: reduce_slabs sums them in a fixed order).  Workgroups of k-tile 0
 //             also emit the column sums of A (= the bias gradient) per split.
 //
@@ -220,7 +220,7 @@ struct NTShape {
   static_assert(ACH % NT == 0, "A chunks per thread must be integral");
 };
 
-template <int WAVES, int RM, int RN, int KT, class AL, class BL, class EP>
+template <int WAVES, int RM, int RN, int KT, int PF, class AL, class BL, class EP>
 __global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N,
                                                              int K, int tiles_n) {
   using S = NTShape<WAVES, RM, RN, KT>;
@@ -266,31 +266,28 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep
     for (int j = 0; j < RN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (K + BK - 1) / BK;
-#pragma unroll
-  for (int p = 0; p < APT; ++p) ra[p] = al.fetch(arow[p], akof[p], K);
-#pragma unroll
-  for (int p = 0; p < BPT; ++p) rb[p] = bl.fetch(brow[p], bkof[p], K);
-#pragma unroll
-  for (int p = 0; p < APT; ++p) As[adst[p]] = al.combine(ra[p], arow[p], akof[p], K);
-#pragma unroll
-  for (int p = 0; p < BPT; ++p)
-    if (bdst[p] >= 0) Bs[bdst[p]] = bl.combine(rb[p], brow[p], bkof[p], K);
-  __syncthreads();
-
   const int fr = lane & 15, fg = lane >> 4;
   const int sw = fg ^ lds_swz(fr);
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    const int kb = (kt + 1) * BK;
-    if (more) {
+
+  auto fetch = [&](typename AL::Raw(&xa)[APT], typename BL::Raw(&xb)[BPT], int kb) {
 #pragma unroll
-      for (int p = 0; p < APT; ++p) ra[p] = al.fetch(arow[p], kb + akof[p], K);
+    for (int p = 0; p < APT; ++p) xa[p] = al.fetch(arow[p], kb + akof[p], K);
 #pragma unroll
-      for (int p = 0; p < BPT; ++p) rb[p] = bl.fetch(brow[p], kb + bkof[p], K);
-    }
-    const float4* Ac = As + cur * ACH;
-    const float4* Bc = Bs + cur * BCH;
+    for (int p = 0; p < BPT; ++p) xb[p] = bl.fetch(brow[p], kb + bkof[p], K);
+  };
+  auto sstore = [&](const typename AL::Raw(&xa)[APT], const typename BL::Raw(&xb)[BPT], int buf,
+                    int kb) {
+    float4* An = As + buf * ACH;
+    float4* Bn = Bs + buf * BCH;
+#pragma unroll
+    for (int p = 0; p < APT; ++p) An[adst[p]] = al.combine(xa[p], arow[p], kb + akof[p], K);
+#pragma unroll
+    for (int p = 0; p < BPT; ++p)
+      if (bdst[p] >= 0) Bn[bdst[p]] = bl.combine(xb[p], brow[p], kb + bkof[p], K);
+  };
+  auto compute = [&](int buf) {
+    const float4* Ac = As + buf * ACH;
+    const float4* Bc = Bs + buf * BCH;
 #pragma unroll
     for (int c16 = 0; c16 < KT; ++c16) {
       float4 a[RM], b[RN];
@@ -307,16 +304,54 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(a[i], s), f4get(b[j], s),
                                                              acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      float4* An = As + (cur ^ 1) * ACH;
-      float4* Bn = Bs + (cur ^ 1) * BCH;
-#pragma unroll
-      for (int p = 0; p < APT; ++p) An[adst[p]] = al.combine(ra[p], arow[p], kb + akof[p], K);
-#pragma unroll
-      for (int p = 0; p < BPT; ++p)
-        if (bdst[p] >= 0) Bn[bdst[p]] = bl.combine(rb[p], brow[p], kb + bkof[p], K);
-    }
+  };
+
+  if constexpr (PF == 1) {
+    fetch(ra, rb, 0);
+    sstore(ra, rb, 0, 0);
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      const int kb = (kt + 1) * BK;
+      if (more) fetch(ra, rb, kb);
+      compute(cur);
+      if (more) sstore(ra, rb, cur ^ 1, kb);
+      __syncthreads();
+    }
+  } else {
+    // prefetch distance 2: the global loads of tile t+2 are issued before tile t is computed and
+    // consumed (written to LDS) only at the end of iteration t+1, so each load has two
+    // iterations of MFMA work to land.  Register sets alternate by tile parity (loop unrolled
+    // by 2 so they stay static); two LDS buffers suffice because a buffer is rewritten only
+    // after the barrier that ends its readers' iteration.
+    // Fetches are unconditional (tiles past K read in-bounds addresses and are zero-masked by
+    // combine), so no branch separates a load from its consumer and the waitcnt pass can count.
+    typename AL::Raw ra2[APT];
+    typename BL::Raw rb2[BPT];
+    fetch(ra, rb, 0);
+    fetch(ra2, rb2, BK);
+    sstore(ra, rb, 0, 0);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 2 <= nk; kt += 2) {  // buf 0 holds tile kt, set 2 holds tile kt + 1
+      fetch(ra, rb, (kt + 2) * BK);
+      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
+      sstore(ra2, rb2, 1, (kt + 1) * BK);
+      __syncthreads();
+      fetch(ra2, rb2, (kt + 3) * BK);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      __builtin_amdgcn_sched_barrier(0);
+      sstore(ra, rb, 0, (kt + 2) * BK);
+      __syncthreads();
+    }
+    if (kt < nk) {
+      compute(0);
+      __syncthreads();  // the epilogue reuses the stage buffers
+    }
   }
 
   // epilogue: accumulators -> LDS [BM][LDC] -> coalesced float4 rows -> ep.apply4
@@ -337,13 +372,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep
   }
 }
 
-template <int WAVES, int RM, int RN, int KT, class AL, class BL, class EP>
+template <int WAVES, int RM, int RN, int KT, class AL, class BL, class EP, int PF = 2>
 inline hipError_t launch_gemm_nt(const AL& al, const BL& bl, const EP& ep, int M, int N, int K,
                                  hipStream_t st) {
   using S = NTShape<WAVES, RM, RN, KT>;
   if (M <= 0 || N <= 0) return hipSuccess;
   const int tm = (M + S::BM - 1) / S::BM, tn = (N + S::BN - 1) / S::BN;
-  hipLaunchKernelGGL((gemm_nt_kernel<WAVES, RM, RN, KT, AL, BL, EP>), dim3(tm * tn),
+  hipLaunchKernelGGL((gemm_nt_kernel<WAVES, RM, RN, KT, PF, AL, BL, EP>), dim3(tm * tn),
                      dim3(WAVES * 64), 0, st, al, bl, ep, M, N, K, tn);
   return hipGetLastError();
 }
@@ -383,10 +418,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
   float* Bt = lds + 2 * BE * SA;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  // 1-D grid of tiles x splits; the XCD-contiguous remap puts all output tiles of one split (which
+  // read the same rows) on one XCD, so their re-reads of those rows hit that XCD's L2
+  const int ntiles = ((Nout + BM - 1) / BM) * tiles_k;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / ntiles, tile = lin - split * ntiles;
   const int tnn = tile / tiles_k, tkk = tile - tnn * tiles_k;
   const int n0 = tnn * BM, k0 = tkk * BN;
-  const int split = blockIdx.y;
   const int e_begin = split * rows_per_split;
   const int e_end = min(R, e_begin + rows_per_split);
   const int nt = e_end > e_begin ? (e_end - e_begin + BE - 1) / BE : 0;
@@ -503,23 +541,16 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
       for (int r = 0; r < 4; ++r)
         C[(w * 16 * RM + i * 16 + fg * 4 + r) * S::LDC + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
-  float* out = slab + (int64_t)split * Nout * Kout;
+  // slab rows are padded to ldk = round_up(Kout, 4) floats so every store is a float4
+  const int ldk = (Kout + 3) & ~3;
+  float* out = slab + (int64_t)split * Nout * ldk;
   constexpr int C4 = BN / 4;
-  const bool vec_ok = (Kout & 3) == 0;
   for (int q = tid; q < BM * C4; q += NT) {
     const int r = q / C4, c4 = q - r * C4;
     const int row = n0 + r, col = k0 + 4 * c4;
     if (row >= Nout || col >= Kout) continue;
-    const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
-    float* o = out + (int64_t)row * Kout + col;
-    if (vec_ok && col + 4 <= Kout) {
-      *reinterpret_cast<float4*>(o) = v;
-    } else {
-      o[0] = v.x;
-      if (col + 1 < Kout) o[1] = v.y;
-      if (col + 2 < Kout) o[2] = v.z;
-      if (col + 3 < Kout) o[3] = v.w;
-    }
+    *reinterpret_cast<float4*>(out + (int64_t)row * ldk + col) =
+        *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
   }
   if (do_bias && n0 + tid < Nout) bslab[(int64_t)split * Nout + n0 + tid] = bsum;
 }
@@ -547,7 +578,7 @@ inline hipError_t launch_gemm_tn(const AL& al, const BL& bl, const TnPlan& p, fl
                                  float* bslab, int Nout, int Kout, int R, bool want_bias,
                                  hipStream_t st) {
   hipLaunchKernelGGL((gemm_tn_kernel<WAVES, RM, RN, KT, AL, BL>),
-                     dim3(p.tiles_n * p.tiles_k, p.splits), dim3(WAVES * 64), 0, st, al, bl, slab,
+                     dim3(p.tiles_n * p.tiles_k * p.splits), dim3(WAVES * 64), 0, st, al, bl, slab,
                      bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
   return hipGetLastError();
 }

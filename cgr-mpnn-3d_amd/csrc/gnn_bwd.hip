@@ -30,11 +30,11 @@ namespace cgr {
 void dropout_params(const float* dropout_p, int training, int l, uint32_t* thresh, float* scale);
 
 template <class AL, class BL>
-static hipError_t tn_gemm(const AL& al, const BL& bl, int Nout, int Kout, int R, float* slab,
-                          float* bslab, bool want_bias, TnPlan* plan, hipStream_t st) {
+static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout, int Kout, int R,
+                          float* slab, float* bslab, bool want_bias, TnPlan* plan, hipStream_t st) {
   *plan = tn_plan(Nout, Kout, R);
   const TnPlan p = *plan;
-  ProfScope _p("gemm_tn_wgrad", st);
+  ProfScope _p(name, st);
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
     return launch_gemm_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(al, bl, p, slab, bslab,
                                                                          Nout, Kout, R, want_bias,
@@ -107,7 +107,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     hipError_t e = with_vec(vx, [&](auto VX) {
       LdPlain<4> al{dzn, Hp};
       LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
-      return tn_gemm(al, bl, H, F + H, N, slab, bslab, true, &p, side);
+      return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, slab, bslab, true, &p, side);
     });
     HIP_RET(e);
     HIP_RET(tn_reduce(p, slab, bslab, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
@@ -115,7 +115,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   }
   // main: ds = dzn W_n[:, F:]
   {
-    ProfScope _p("gemm_nt_bwd", st);
+    ProfScope _p("gemm_nt_readout_bwd", st);
     hipError_t e = with_nt_rn(H, [&](auto RN) {
       LdPlain<4> al{dzn, Hp};
       LdPlain<4> bl{wT + D * HHp, Hp};
@@ -143,7 +143,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.pre = fv.pre[l + 1];
     la.h0 = fv.h[0];
     la.sigma = d.learnable_skip ? params[CGR_PARAM_SKIP(D, l)] : nullptr;
-    la.seed = seed;
+    la.seed = iv.rng;  // the key the forward used (arena)
     la.thresh = thresh;
     la.scale = scale;
     la.layer = l;
@@ -165,14 +165,14 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dp, Hp};
       LdGatherDiff<false> bl{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
       TnPlan p;
-      HIP_RET(tn_gemm(al, bl, H, H, E, slab, bslab, true, &p, side));
+      HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, slab, bslab, true, &p, side));
       HIP_RET(record_point(ss, side, &tn_done[l]));
       HIP_RET(tn_reduce(p, slab, bslab, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
                         grads[CGR_PARAM_CONV_B(l)], side));
     }
     // main: dm = dpre W_l ; da[v] = sum_{src(e) = v} dm[e]
     {
-      ProfScope _p("gemm_nt_bwd", st);
+      ProfScope _p("gemm_nt_layer_bwd", st);
       hipError_t e = with_nt_rn(H, [&](auto RN) {
         LdPlain<4> al{dp, Hp};
         LdPlain<4> bl{wT + l * HHp, Hp};
@@ -201,7 +201,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     LdPlain<4> al{dpre0, Hp};
     LdPlain<4> bl{fv.e_s, d.Fep};
     TnPlan p;
-    HIP_RET(tn_gemm(al, bl, H, Fe, E, slab, bslab, true, &p, side));
+    HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, slab, bslab, true, &p, side));
     HIP_RET(tn_reduce(p, slab, bslab, H, Fe, gW0, F + Fe, F, gb0, side));
   }
   {
@@ -214,7 +214,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     hipError_t e = with_vec(vx, [&](auto VX) {
       LdPlain<4> al{Gs, Hp};
       LdPlain<decltype(VX)::value> bl{b->x, F};
-      return tn_gemm(al, bl, H, F, N, slab2, bslab2, Fe == 0, &p, st);
+      return tn_gemm("gemm_tn_wgrad_node", al, bl, H, F, N, slab2, bslab2, Fe == 0, &p, st);
     });
     HIP_RET(e);
     HIP_RET(tn_reduce(p, slab2, bslab2, H, F, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st));

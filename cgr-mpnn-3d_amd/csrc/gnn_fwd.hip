@@ -44,8 +44,8 @@ void dropout_params(const float* dropout_p, int training, int l, uint32_t* thres
 }
 
 int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
-                     const float* dropout_p, uint64_t seed, int training, void* arena, float* y,
-                     hipStream_t st) {
+                     const float* dropout_p, uint64_t seed, uint64_t* rng_counter, int training,
+                     void* arena, float* y, hipStream_t st) {
   const ArenaLayout L = arena_layout(d);
   const IndexView iv = index_view(arena, L);
   const FloatView fv = float_view(arena, L, d);
@@ -54,6 +54,16 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   const float* b0 = params[CGR_PARAM_EDGE_INIT_B];
   const float* Wn = params[CGR_PARAM_E2N_W(D)];
   const float* bn = params[CGR_PARAM_E2N_B(D)];
+
+  // dropout key of this forward -> arena (the backward and every epilogue read it from there)
+  bool any_dropout = false;
+  for (int l = 0; l < D; ++l) {
+    uint32_t t;
+    float s;
+    dropout_consts(dropout_p, training, l, &t, &s);
+    any_dropout = any_dropout || t != 0;
+  }
+  if (any_dropout) HIP_RET(rng_key(seed, rng_counter, iv.rng, st));
 
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
@@ -122,7 +132,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
                fv.pre[l + 1], Hp,
                E,        H,
                d.act,    thresh,
-               scale,    seed,
+               scale,    iv.rng,
                l};
     LdGatherDiff<false> al{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
     {

@@ -42,6 +42,7 @@ struct IndexView {
   int* cursor2;
   int* graph_cnt;
   int* status;
+  uint64_t* rng;  // effective dropout key of this forward (read by every dropout kernel)
   void* zero_block;
   size_t zero_bytes;
   int* perm;
@@ -83,7 +84,7 @@ struct ArenaLayout {
   size_t off_index_begin;
   size_t bytes;
   // offsets (bytes) for every buffer
-  size_t zero_block, zero_bytes, deg_dst, deg_src, cursor, cursor2, graph_cnt, status;
+  size_t zero_block, zero_bytes, deg_dst, deg_src, cursor, cursor2, graph_cnt, status, rng;
   size_t perm, src_s, dst_s, rev_s, src_list, inv, src_c, dst_c, dst_ptr, src_ptr, graph_ptr,
       node_graph;
   size_t e_s, w0eT, P, Q, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,

@@ -303,6 +303,7 @@ __global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
                  *reinterpret_cast<const float4*>(a.dm + (int64_t)a.rev_s[i] * a.Hp + n));
     }
     float d[4] = {dh.x, dh.y, dh.z, dh.w};
+    const uint64_t key = a.thresh ? *a.seed : 0;
     if (a.act == ACT_RELU) {
       const float4 hv = *reinterpret_cast<const float4*>(a.hnext + o);
       const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
@@ -315,7 +316,7 @@ __global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
       for (int k = 0; k < 4; ++k) {
         float m = a.scale;
         if (a.thresh && n + k < a.H)
-          m = drop_keep(a.seed, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
+          m = drop_keep(key, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
                                                                                         : 0.f;
         d[k] = d[k] * m * act_grad(zz[k], a.act);
       }
@@ -395,24 +396,58 @@ hipError_t edge_init_bwd(const float* dh0, const float* da, const float* dm, con
 }
 
 // ------------------------------------------------------------------------------------------
+// dropout key (graph-safe: the counter lives on the device and advances per forward)
+// ------------------------------------------------------------------------------------------
+__global__ void k_rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out) {
+  uint64_t k = seed;
+  if (counter) {
+    const uint64_t c = counter[0];
+    k = seed + 0xD1B54A32D192ED03ull * (c + 1);
+    counter[0] = c + 1;
+  }
+  key_out[0] = k;
+}
+
+hipError_t rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out, hipStream_t st) {
+  hipLaunchKernelGGL(k_rng_key, dim3(1), dim3(1), 0, st, seed, counter, key_out);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // deterministic split-K reduction of weight-gradient slabs
 // ------------------------------------------------------------------------------------------
+// slab layout [splits][Nout][ldk], ldk = round_up(Kout, 4) (gemm_tn_kernel): one thread per float4
+// of a slab row, 16-byte loads of every split in a fixed order (deterministic).
 __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ slab,
                                                       const float* __restrict__ bslab, int splits,
                                                       int Nout, int Kout, float* __restrict__ dst,
                                                       int64_t ld_dst, int64_t col_off,
                                                       float* __restrict__ bias_dst) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t nk = (int64_t)Nout * Kout;
-  if (t < nk) {
-    const int64_t n = t / Kout, k = t - n * Kout;
-    float s = 0.f;
-    // fixed summation order (deterministic); unrolled so the loads of 8 splits are in flight
+  const int ldk = (Kout + 3) & ~3;
+  const int c4n = ldk >> 2;
+  const int64_t nf = (int64_t)Nout * c4n;
+  const int64_t split_f4 = (int64_t)Nout * c4n;  // float4 per split
+  if (t < nf) {
+    const int64_t n = t / c4n;
+    const int k = (int)(t - n * c4n) * 4;
+    const float4* s4 = reinterpret_cast<const float4*>(slab) + t;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 8
-    for (int p = 0; p < splits; ++p) s += slab[(int64_t)p * nk + t];
-    dst[n * ld_dst + col_off + k] = s;
-  } else if (bias_dst && t < nk + Nout) {
-    const int64_t n = t - nk;
+    for (int p = 0; p < splits; ++p) {
+      const float4 v = s4[(int64_t)p * split_f4];
+      s.x += v.x;
+      s.y += v.y;
+      s.z += v.z;
+      s.w += v.w;
+    }
+    float* o = dst + n * ld_dst + col_off + k;
+    o[0] = s.x;
+    if (k + 1 < Kout) o[1] = s.y;
+    if (k + 2 < Kout) o[2] = s.z;
+    if (k + 3 < Kout) o[3] = s.w;
+  } else if (bias_dst && t < nf + Nout) {
+    const int64_t n = t - nf;
     float s = 0.f;
     for (int p = 0; p < splits; ++p) s += bslab[(int64_t)p * Nout + n];
     bias_dst[n] = s;
@@ -422,7 +457,7 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                         hipStream_t st) {
-  const int64_t tot = (int64_t)Nout * Kout + (bias_dst ? Nout : 0);
+  const int64_t tot = (int64_t)Nout * (((Kout + 3) & ~3) >> 2) + (bias_dst ? Nout : 0);
   if (tot <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(tot, 256)), dim3(256), 0, st, slab, bslab, splits,
                      Nout, Kout, dst, ld_dst, col_off, bias_dst);

@@ -7,6 +7,9 @@
 namespace cgr {
 
 // out[s, :w] = sum_{j in [ptr[s], ptr[s+1])} vals[idx ? idx[j] : j, :w]
+// dropout key of one forward: key = seed (+ a Weyl step per *counter, which is then incremented)
+hipError_t rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out, hipStream_t st);
+
 hipError_t segment_sum(const float* vals, int64_t ldv, const int* idx, const int* ptr,
                        int64_t nseg, int64_t width, float* out, int64_t ldo, hipStream_t st);
 
@@ -54,7 +57,7 @@ struct LayerBwdArgs {
   const float* pre;    // pre_{l} (non-ReLU)
   const float* h0;
   const float* sigma;  // skip weight (nullptr -> 1)
-  uint64_t seed;
+  const uint64_t* seed;  // device dropout key (arena "rng")
   uint32_t thresh;
   float scale;
   int layer;

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CGR_ABI_VERSION 1
+#define CGR_ABI_VERSION 2
 #define CGR_MAX_DEPTH 32
 
 enum cgr_status {
@@ -97,7 +97,7 @@ int64_t cgr_gnn_arena_bytes(const cgr_gnn_config* cfg, int64_t num_nodes, int64_
 int64_t cgr_gnn_workspace_bytes(const cgr_gnn_config* cfg, int64_t num_nodes, int64_t num_edges,
                                 int64_t num_graphs);
 
-/* Byte offset of a named arena buffer (introspection for tests/debugging).  Names: "status",
+/* Byte offset of a named arena buffer (introspection for tests/debugging).  Names: "status", "rng",
  * "perm", "src_s", "dst_s", "rev_s", "src_list", "dst_ptr", "src_ptr", "graph_ptr",
  * "node_graph", "e_s", "P", "h", "a", "pre", "zn", "hn", "g"; `index` selects the layer for
  * "h" / "a" / "pre".  Returns -1 for an unknown or absent buffer. */
@@ -112,11 +112,14 @@ int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* batch, void* aren
 /* GNN.forward(data) -> [B] (GNN.py:76-110): edge init, `depth` fused D-MPNN layers
  * (gather -> MFMA GEMM -> bias/skip/act/dropout epilogue -> segmented reduce), edge->node
  * readout, add-pool and ffn.  Dropout (GNN.py:100-102) is applied when `training` != 0 and
- * dropout_p[l] > 0, from a counter-based RNG keyed by `seed`.  Fills `arena` with what
- * cgr_gnn_backward needs.  `y` device [B]. */
+ * dropout_p[l] > 0, from a counter-based RNG keyed by `seed` and, when `rng_counter` (device
+ * uint64, may be NULL) is given, by its value, which the forward then increments on the device:
+ * a captured graph replays with a fresh mask each time (the key is kept in the arena for the
+ * backward).  Fills `arena` with what cgr_gnn_backward needs.  `y` device [B]. */
 int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params,
                     const cgr_batch* batch, const float* dropout_p, uint64_t seed,
-                    int32_t training, void* arena, float* y, void* stream);
+                    uint64_t* rng_counter, int32_t training, void* arena, float* y,
+                    void* stream);
 
 /* Reverse mode of cgr_gnn_forward (what autograd runs for the reference: GNN.py:76-145 under
  * loss.backward(), trainer.py:142-143).  `dy` device [B] = dLoss/dy; writes every parameter
@@ -149,6 +152,30 @@ int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t num_nodes, int64_
                             const float* h, int64_t hidden, const float* weight,
                             const float* grad_a, const float* grad_h_out, float* grad_h,
                             float* grad_weight, float* grad_bias, void* scratch, void* stream);
+
+/* torch.optim.Adam(params, lr, betas, eps, weight_decay, amsgrad) step (train.py:117-119), fused
+ * over every parameter tensor in one launch (+ one tiny launch for the step counter) instead of
+ * the ~11 multi-tensor launches of torch's foreach path.  Per element, in the rounding order of
+ * torch/optim/adam.py _multi_tensor_adam (hyper-parameters as Python doubles):
+ *   g = grad (+ weight_decay * p);  m += (1 - b1) (g - m);  v = b2 v + (1 - b2) g^2;
+ *   vmax = max(vmax, v) (amsgrad);  p -= lr / (1 - b1^t) * m / (sqrt(vmax or v) / sqrt(1 - b2^t) + eps)
+ * with t = *step + 1 written back to *step: a per-tensor device float, like torch's state["step"]
+ * (capturable=True), so a captured graph replays with the right bias corrections.  grad == NULL
+ * skips a tensor and leaves its step (p.grad is None).  max_exp_avg_sq may be NULL when
+ * amsgrad == 0.  Any number of tensors (launched in groups of CGR_ADAM_GROUP). */
+#define CGR_ADAM_GROUP 32
+typedef struct cgr_adam_tensor {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  float* max_exp_avg_sq;
+  float* step; /* device scalar */
+  int64_t numel;
+} cgr_adam_tensor;
+int cgr_adam_step(const cgr_adam_tensor* tensors, int32_t num_tensors, double lr, double beta1,
+                  double beta2, double eps, double weight_decay, int32_t amsgrad,
+                  int32_t maximize, void* stream);
 
 /* Instrumentation (no reference counterpart): per-kernel-class device time measured with HIP
  * events recorded on the launch stream around every launch of cgr_gnn_forward/_backward.

@@ -83,8 +83,24 @@ def test_invalid_batch_rejected_before_any_launch():
     # odd edge count: the reference's view(E//2, 2, -1) needs pairs
     b = native.CgrBatch(1, 1, 1, None, None, 4, 3, 1)
     params = (ctypes.c_void_p * 8)(*([1] * 8))
-    rc = lib.cgr_gnn_forward(ctypes.byref(c), params, ctypes.byref(b), None, 0, 0, 1, 1, None)
+    rc = lib.cgr_gnn_forward(ctypes.byref(c), params, ctypes.byref(b), None, 0, None, 0, 1, 1,
+                             None)
     assert rc == 1 and b"even" in lib.cgr_last_error()
     b = native.CgrBatch(1, 1, 1, None, None, 4, 4, 2)  # B > 1 but no batch vector
-    rc = lib.cgr_gnn_forward(ctypes.byref(c), params, ctypes.byref(b), None, 0, 0, 1, 1, None)
+    rc = lib.cgr_gnn_forward(ctypes.byref(c), params, ctypes.byref(b), None, 0, None, 0, 1, 1,
+                             None)
     assert rc == 1
+
+
+def test_fused_adam_rejects_cpu_parameters():
+    import torch
+
+    from cgr_mpnn_3D._amd.optim import FusedAdam
+
+    p = torch.zeros(4, requires_grad=True)
+    opt = FusedAdam([p], lr=1e-3, amsgrad=True)
+    p.grad = torch.ones(4)
+    with pytest.raises(RuntimeError, match="GPU"):
+        opt.step()
+    with pytest.raises(ValueError):
+        FusedAdam([p], lr=-1.0)

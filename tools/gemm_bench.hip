@@ -13,7 +13,7 @@
 
 #include "../cgr-mpnn-3d_amd/csrc/epilogues.hpp"
 #include "../cgr-mpnn-3d_amd/csrc/gemm.hpp"
-#include "../cgr-mpnn-3d_amd/csrc/gemm_ws.hpp"
+#include "../cgr-mpnn-3d_amd/csrc/gemm_dma.hpp"
 
 using namespace cgr;
 
@@ -81,18 +81,54 @@ int main(int argc, char** argv) {
   LdGatherDiff<false> gd{a, h, dsrc, drev, Hp};
   LdPlain<4> wl{W, H};
   float* ref_nt = nullptr;
-#define NTV(W_, RM_, RN_, KT_)                                                                    \
+#define NTV(W_, RM_, RN_, KT_, PF_)                                                                  \
   {                                                                                               \
     float* o = out_buf((size_t)E * Hp);                                                           \
     EpLayer ep{bias, nullptr, h0, o, nullptr, Hp, E, H, ACT_RELU, 0u, 1.f, 0, 0};                 \
-    vs.push_back({"nt<" #W_ "," #RM_ "," #RN_ "," #KT_ ">", fl_layer,                            \
+    vs.push_back({"nt<" #W_ "," #RM_ "," #RN_ "," #KT_ "> pf" #PF_, fl_layer,                   \
                   [=](hipStream_t s) {                                                            \
-                    (void)launch_gemm_nt<W_, RM_, RN_, KT_>(gd, wl, ep, E, H, H, s);              \
+                    (void)launch_gemm_nt<W_, RM_, RN_, KT_, decltype(gd), decltype(wl), EpLayer, PF_>(gd, wl, ep, E, H, H, s);           \
                   },                                                                              \
                   o, (size_t)E * Hp, ref_nt});                                                    \
     if (!ref_nt) ref_nt = o;                                                                      \
   }
-  NTV(4, 1, 5, 1)
+  NTV(4, 1, 5, 1, 1)
+  NTV(4, 1, 5, 1, 2)
+  NTV(8, 1, 13, 1, 1)
+  {
+    float* o = out_buf((size_t)E * Hp);
+    EpLayer ep{bias, nullptr, h0, o, nullptr, Hp, E, H, ACT_RELU, 0u, 1.f, 0, 0};
+    DmaA da{a, h, dsrc, drev, Hp};
+    vs.push_back({"dma<5,5,1,gather>", fl_layer,
+                  [=](hipStream_t s) {
+                    (void)launch_gemm_nt_dma<5, 5, 1, true>(da, W, H, ep, E, H, H, s);
+                  },
+                  o, (size_t)E * Hp, ref_nt});
+  }
+  // plain-A NT (dm = dpre W): register-staged vs DMA
+  float* dpre0 = dev_rand((size_t)E * Hp, 12);
+  float* ref_pl = nullptr;
+  {
+    float* o = out_buf((size_t)E * Hp);
+    EpStore ep{o, Hp, E, H, nullptr};
+    LdPlain<4> ap{dpre0, Hp};
+    vs.push_back({"plain nt<4,1,5,1> pf1", fl_layer,
+                  [=](hipStream_t s) {
+                    (void)launch_gemm_nt<4, 1, 5, 1, LdPlain<4>, LdPlain<4>, EpStore, 1>(ap, wl, ep, E, H, H, s);
+                  },
+                  o, (size_t)E * Hp, nullptr});
+    ref_pl = o;
+  }
+  {
+    float* o = out_buf((size_t)E * Hp);
+    EpStore ep{o, Hp, E, H, nullptr};
+    DmaA da{dpre0, nullptr, nullptr, nullptr, Hp};
+    vs.push_back({"plain dma<5,5,1>", fl_layer,
+                  [=](hipStream_t s) {
+                    (void)launch_gemm_nt_dma<5, 5, 1, false>(da, W, H, ep, E, H, H, s);
+                  },
+                  o, (size_t)E * Hp, ref_pl});
+  }
   int ncu = 256;
   {
     hipDeviceProp_t prop;
@@ -110,11 +146,6 @@ int main(int argc, char** argv) {
                   },                                                                              \
                   o, (size_t)E * Hp, ref_nt});                                                    \
   }
-  WSV(5, 5, 1)
-  WSV(5, 1, 1)
-  WSV(5, 3, 1)
-  WSV(4, 4, 1)
-  WSV(5, 5, 2)
   // ---- TN layer weight gradient (dpre^T m) ----
   float* dpre = dev_rand((size_t)E * Hp, 11);
   LdPlain<4> ad{dpre, Hp};
@@ -133,31 +164,23 @@ int main(int argc, char** argv) {
                   slab, 0, nullptr});                                                         \
   }
   TNV(5, 1, 5, 1, 1024)
-  TNV(5, 1, 5, 2, 1024)
-  TNV(5, 1, 5, 2, 512)
-  TNV(5, 2, 5, 1, 1024)
-  TNV(5, 2, 5, 2, 512)
-  TNV(5, 1, 5, 4, 256)
   // ---- NT readout (x | s) ----
   const double fl_ro = 2.0 * N * (F + H) * H;
   LdConcat<2> cc{x, F, a, Hp, F};
   LdPlain<2> wn{Wn, F + H};
   float* ref_ro = nullptr;
-#define ROV(W_, RM_, RN_, KT_)                                                                \
+#define ROV(W_, RM_, RN_, KT_, PF_)                                                               \
   {                                                                                           \
     float* o = out_buf((size_t)N * Hp);                                                       \
     EpReadout ep{bias, o, nullptr, Hp, N, H, ACT_RELU};                                       \
-    vs.push_back({"ro<" #W_ "," #RM_ "," #RN_ "," #KT_ ">", fl_ro,                           \
+    vs.push_back({"ro<" #W_ "," #RM_ "," #RN_ "," #KT_ "> pf" #PF_, fl_ro,                  \
                   [=](hipStream_t s) {                                                        \
-                    (void)launch_gemm_nt<W_, RM_, RN_, KT_>(cc, wn, ep, N, H, F + H, s);      \
+                    (void)launch_gemm_nt<W_, RM_, RN_, KT_, decltype(cc), decltype(wn), EpReadout, PF_>(cc, wn, ep, N, H, F + H, s);      \
                   },                                                                          \
                   o, (size_t)N * Hp, ref_ro});                                                \
     if (!ref_ro) ref_ro = o;                                                                  \
   }
-  ROV(4, 1, 5, 1)
-  ROV(4, 1, 5, 2)
-  ROV(4, 2, 5, 2)
-  ROV(8, 1, 5, 2)
+  ROV(4, 1, 5, 2, 1)
 
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
