@@ -30,8 +30,10 @@ fi
 
 if [ "${SKIP_PROF:-0}" = "0" ]; then
   stage "rocprofv3 kernel trace"
+  # the bench command itself (graph-captured timed steps + the serial instrumented pass), so the
+  # per-kernel averages here can be set against the bench line's roofline entry
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-    -- python bench.py --steps 20 --warmup 3 --cpu-baseline 0 --graph 0 --profile-steps 0 \
+    -- python bench.py --steps 20 --warmup 3 --cpu-baseline 0 ${PROF_ARGS:-} \
     > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err"
   rc=$?; stage "rocprof rc=$rc"
   find "$OUT/prof" -name "*stats*" | head
