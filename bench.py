@@ -117,6 +117,54 @@ def roofline_entry(name, work, launches, ms_total, traffic):
             "timing": "HIP events on the launch stream, instrumented serial pass"}
 
 
+def scatter_add_roofline(edge_index, N, H, dev, reps=50):
+    """The path's scatter-add (PyG propagate aggr='add', GNN.py:134) as the native forward runs
+    it -- cgr_segment_sum over the dst-sorted edge rows [E, H] into [N, H] -- and its backward
+    twin (rows gathered through the src permutation), each timed as `reps` back-to-back launches
+    between two HIP events on the launch stream (a single ~8 us launch between events also
+    times the event/dispatch gap).  Inputs are HBM-resident, sized like the bench batch."""
+    from cgr_mpnn_3D._amd import native
+
+    lib = native.load()
+    E = edge_index.shape[1]
+    src, dst = edge_index[0], edge_index[1]
+    vals = torch.randn(E, H, device=dev)
+    out = torch.empty(N, H, device=dev)
+
+    def csr(keys):
+        deg = torch.bincount(keys, minlength=N)
+        ptr = torch.zeros(N + 1, dtype=torch.int32, device=dev)
+        ptr[1:] = torch.cumsum(deg, 0).to(torch.int32)
+        return ptr
+
+    ptr_dst = csr(dst)
+    ptr_src = csr(src)
+    perm_src = torch.argsort(src, stable=True).to(torch.int32)
+    stream = torch.cuda.current_stream(dev)
+    res = {}
+    for name, idx, ptr in (("segsum_dst_fwd", None, ptr_dst), ("segsum_src_bwd", perm_src, ptr_src)):
+        def launch():
+            native.check(lib.cgr_segment_sum(native.ptr(vals), H, native.ptr(idx), native.ptr(ptr),
+                                             N, H, native.ptr(out), H, stream.cuda_stream))
+        for _ in range(5):
+            launch()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            launch()
+        e1.record(stream)
+        e1.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / reps
+        nbytes = 4.0 * (E * H + N * H) + 4.0 * (N + 1) + (4.0 * E if idx is not None else 0.0)
+        res[name] = {"kernel": name, "bound": "hbm", "achieved": round(nbytes / us / 1e3, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes_per_launch": nbytes, "avg_launch_us": round(us, 3),
+                     "timing": f"{reps} back-to-back cgr_segment_sum launches between HIP events "
+                               f"on the launch stream, E={E} rows x H={H} -> N={N}"}
+    return res
+
+
 # ------------------------------------------------------------------------------------------------
 def cpu_baseline(cfgname, seconds, dropout):
     """Reference CPU path (oracle/dmpnn_torch.py: the reference ATen op sequence incl. its dead
@@ -284,10 +332,10 @@ def main():
         if cands:
             dom = max(cands, key=lambda k: rep[k][1])
             roof = roofline_entry(dom, work[dom], rep[dom][0], rep[dom][1], hbm(dom))
-        if "segsum_dst_fwd" in rep:
-            roof_scatter = roofline_entry("segsum_dst_fwd", work["segsum_dst_fwd"],
-                                          rep["segsum_dst_fwd"][0], rep["segsum_dst_fwd"][1],
-                                          hbm("segsum_dst_fwd"))
+        sc = scatter_add_roofline(data.edge_index, N, H, dev)
+        roof_scatter = sc["segsum_dst_fwd"]
+        roof_scatter["traffic"] = hbm("segsum_dst_fwd")
+        roof_scatter["backward_gather_twin"] = sc["segsum_src_bwd"]
         roof_all = {k: roofline_entry(k, work[k], rep[k][0], rep[k][1], hbm(k))["frac"]
                     for k in cands}
 

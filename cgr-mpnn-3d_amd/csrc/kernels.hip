@@ -10,6 +10,9 @@ namespace cgr {
 // ------------------------------------------------------------------------------------------
 // segmented sum
 // ------------------------------------------------------------------------------------------
+// one thread per (segment, float4 column); rows are summed in index order (deterministic), but
+// the loads of up to 4 rows are issued together (a runtime-trip-count loop would serialise them:
+// ptr -> row -> add -> next row); segments average ~2 rows on T1x-shaped graphs
 template <bool GATHER>
 __global__ __launch_bounds__(256) void k_segsum_v4(const float* __restrict__ vals, int64_t ldv,
                                                    const int* __restrict__ idx,
@@ -20,10 +23,23 @@ __global__ __launch_bounds__(256) void k_segsum_v4(const float* __restrict__ val
   const int64_t v = t / C4;
   const int c = (int)(t - v * C4);
   const int b = ptr[v], e = ptr[v + 1];
+  const float* base = vals + 4 * c;
+  auto row = [&](int j) -> int64_t { return GATHER ? (int64_t)idx[j] : (int64_t)j; };
+  auto ld = [&](int64_t r) { return *reinterpret_cast<const float4*>(base + r * ldv); };
   float4 acc = f4zero();
-  for (int j = b; j < e; ++j) {
-    const int64_t row = GATHER ? idx[j] : j;
-    acc = f4add(acc, *reinterpret_cast<const float4*>(vals + row * ldv + 4 * c));
+  int j = b;
+  for (; j + 4 <= e; j += 4) {
+    const int64_t r0 = row(j), r1 = row(j + 1), r2 = row(j + 2), r3 = row(j + 3);
+    const float4 x0 = ld(r0), x1 = ld(r1), x2 = ld(r2), x3 = ld(r3);
+    acc = f4add(f4add(f4add(f4add(acc, x0), x1), x2), x3);
+  }
+  const int rem = e - j;
+  if (rem > 0) {  // 1..3 rows: clamped (always valid) loads, predicated adds
+    const int64_t r0 = row(j), r1 = row(min(j + 1, e - 1)), r2 = row(min(j + 2, e - 1));
+    const float4 x0 = ld(r0), x1 = ld(r1), x2 = ld(r2);
+    acc = f4add(acc, x0);
+    if (rem > 1) acc = f4add(acc, x1);
+    if (rem > 2) acc = f4add(acc, x2);
   }
   *reinterpret_cast<float4*>(out + v * ldo + 4 * c) = acc;
 }

@@ -67,14 +67,24 @@ __global__ __launch_bounds__(WAVES * 64) void probe(const float* __restrict__ A,
   __syncthreads();
   const int fr = lane & 15, fg = lane >> 4, sw = fg ^ lds_swz(fr);
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = (MODE == 3) ? 0 : (kt & 1);
+    const int cur = (MODE == 3 || MODE == 5) ? 0 : (kt & 1);
     const bool more = kt + 1 < nk;
     const int kb = (kt + 1) * 16 * KT;
-    if (MODE != 1 && MODE != 3 && more) {
+    if (MODE != 1 && MODE != 3 && MODE != 5 && more) {  // MODE 6/7: loads + register MFMAs
       for (int p = 0; p < APT; ++p) ra[p] = *reinterpret_cast<const float4*>(ap[p] + kb + akof[p]);
       for (int p = 0; p < BPT; ++p) rb[p] = *reinterpret_cast<const float4*>(bp[p] + kb + bkof[p]);
     }
-    if (MODE != 2) {
+    if (MODE == 5 || MODE == 6 || MODE == 7) {  // MFMA from registers (6/7: beside the loads)
+      float4 a = ra[0], b0 = rb[0];
+#pragma unroll
+      for (int c = 0; c < KT; ++c)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(a, s), f4get(b0, s), acc[j], 0, 0,
+                                                          0);
+    } else if (MODE != 2) {
 #pragma unroll
       for (int c = 0; c < KT; ++c) {
         const float4* Ac = As + cur * ACH + c * BM * 4;
@@ -89,7 +99,20 @@ __global__ __launch_bounds__(WAVES * 64) void probe(const float* __restrict__ A,
                                                           0, 0);
       }
     }
-    if (MODE != 3) {
+    if (MODE == 6) {  // consume the loads (no LDS, no barrier)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    if (MODE == 7) {  // loads -> LDS, barrier, but MFMA operands from registers
+      if (more) {
+        float4* An = As + (cur ^ 1) * ACH;
+        float4* Bn = Bs + (cur ^ 1) * BCH;
+        for (int p = 0; p < APT; ++p) An[adst[p]] = ra[p];
+        for (int p = 0; p < BPT; ++p)
+          if (bdst[p] >= 0) Bn[bdst[p]] = rb[p];
+      }
+      __syncthreads();
+    }
+    if (MODE != 3 && MODE != 5 && MODE != 6 && MODE != 7) {
       if (more) {
         float4* An = As + (cur ^ 1) * ACH;
         float4* Bn = Bs + (cur ^ 1) * BCH;
@@ -100,7 +123,7 @@ __global__ __launch_bounds__(WAVES * 64) void probe(const float* __restrict__ A,
       __syncthreads();
     }
   }
-  if (MODE == 2) {  // keep the loads alive
+  if (MODE == 2 || MODE == 6) {  // keep the loads alive
     float s = 0.f;
     for (int p = 0; p < APT; ++p) s += ra[p].x;
     for (int p = 0; p < BPT; ++p) s += rb[p].y;
@@ -149,11 +172,12 @@ int main() {
   CK(hipStreamCreate(&st));
   const double fl = 2.0 * M * N * K;
   for (int round = 0; round < 3; ++round) {
-    printf("K=416  KT=1 full %7.2f  no-mfma %7.2f  mfma-only %7.2f | KT=2 full %7.2f  no-mfma %7.2f  mfma-only %7.2f | w8 KT=2 full %7.2f no-mfma %7.2f\n",
+    printf("KT=1: full %7.2f no-mfma %7.2f mfma+lds %7.2f mfma-regs %7.2f | KT=2: full %7.2f no-mfma %7.2f mfma+lds %7.2f mfma-regs %7.2f loads+regmfma %7.2f\n",
            run<0, 4, 5, 1>(A, B, C, M, N, K, st, 20), run<2, 4, 5, 1>(A, B, C, M, N, K, st, 20),
-           run<3, 4, 5, 1>(A, B, C, M, N, K, st, 20), run<0, 4, 5, 2>(A, B, C, M, N, K, st, 20),
-           run<2, 4, 5, 2>(A, B, C, M, N, K, st, 20), run<3, 4, 5, 2>(A, B, C, M, N, K, st, 20),
-           run<0, 8, 5, 2>(A, B, C, M, N, K, st, 20), run<2, 8, 5, 2>(A, B, C, M, N, K, st, 20));
+           run<3, 4, 5, 1>(A, B, C, M, N, K, st, 20), run<5, 4, 5, 1>(A, B, C, M, N, K, st, 20),
+           run<0, 4, 5, 2>(A, B, C, M, N, K, st, 20), run<2, 4, 5, 2>(A, B, C, M, N, K, st, 20),
+           run<3, 4, 5, 2>(A, B, C, M, N, K, st, 20), run<5, 4, 5, 2>(A, B, C, M, N, K, st, 20),
+           run<6, 4, 5, 2>(A, B, C, M, N, K, st, 20));
   }
   (void)fl;
   return 0;
