@@ -28,6 +28,7 @@ Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
   d.F = cfg->num_node_features;
   d.Fe = cfg->num_edge_features;
   d.Fep = (int)round_up(d.Fe, 4);
+  d.Fp = (int)round_up(d.F, 4);
   d.H = cfg->hidden;
   d.Hp = (int)round_up(d.H, 4);
   d.D = cfg->depth;
@@ -80,6 +81,7 @@ ArenaLayout arena_layout(const Dims& d) {
   L.w0eT = d.Fe ? b.take(4 * (size_t)d.Fe * Hp) : kNone;
   L.P = b.take(4 * N * Hp);
   L.Q = b.take(4 * N * Hp);
+  L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
     L.a[l] = l <= d.D ? b.take(4 * N * Hp) : kNone;
@@ -129,6 +131,7 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.w0eT = (float*)at(arena, L.w0eT);
   f.P = (float*)at(arena, L.P);
   f.Q = (float*)at(arena, L.Q);
+  f.xp = (float*)at(arena, L.xp);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     f.h[l] = (float*)at(arena, L.h[l]);
     f.a[l] = (float*)at(arena, L.a[l]);
@@ -165,7 +168,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   };
   // side-stream TN GEMMs (readout, layers, edge features) share one slab; the main-stream TN
   // (x-part of edge init) runs concurrently with the last of them and gets its own
-  acc(d.H, d.F + d.H, d.N);
+  acc(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N);  // readout TN runs over [xp | s] when padded
   acc(d.H, d.H, d.E);
   if (d.Fe > 0) acc(d.H, d.Fe, d.E);
   W.slab_elems = slab;

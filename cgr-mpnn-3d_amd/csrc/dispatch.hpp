@@ -12,11 +12,12 @@ namespace cgr {
 template <int V>
 using IC = std::integral_constant<int, V>;
 
-// largest of {4, 2, 1} dividing the leading dimension and the logical row length, with a
-// matching pointer alignment
+// widest of {4, 2, 1} such that every row starts VEC-aligned (ld, pointer) and the VEC-wide
+// chunk holding the last logical element stays inside the row (round_up(K, VEC) <= ld): the
+// loaders read whole chunks and mask elements >= K
 inline int vec_for(const void* p, int64_t ld, int64_t K) {
   const uintptr_t a = (uintptr_t)p;
-  if (ld % 4 == 0 && K % 4 == 0 && a % 16 == 0) return 4;
+  if (ld % 4 == 0 && (K + 3) / 4 * 4 <= ld && a % 16 == 0) return 4;
   if (ld % 2 == 0 && K % 2 == 0 && a % 8 == 0) return 2;
   return 1;
 }
@@ -49,7 +50,10 @@ inline auto with_tn_shape(int Nout, int Kout, F&& f) {
   return f(IC<4>{}, IC<4>{});
 }
 
-constexpr int kTnTargetWorkgroups = 1024;  // ~4 per CU on 256 CUs
+#ifndef CGR_TN_TARGET_WGS
+#define CGR_TN_TARGET_WGS 768  // A/B on MI355X (tools/ab_bench.sh): 768 > 1024 > 512 >> 256
+#endif
+constexpr int kTnTargetWorkgroups = CGR_TN_TARGET_WGS;
 
 inline TnPlan tn_plan(int Nout, int Kout, int R) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {

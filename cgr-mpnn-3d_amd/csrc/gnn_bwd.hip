@@ -44,9 +44,10 @@ static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout
 
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
                             int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
-                            hipStream_t st) {
+                            hipStream_t st, int gap_at = 0, int gap_len = 0) {
   ProfScope _p("splitk_reduce", st);
-  return reduce_slabs(slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, st);
+  return reduce_slabs(slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, st,
+                      gap_at, gap_len);
 }
 
 int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
@@ -101,7 +102,15 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   }
   // side: dW_n = dzn^T [x | s], db_n
   HIP_RET(fork_to(ss, st, side));
-  {
+  if (fv.xp) {  // [xp | s] with x padded to Fp: the pad columns are skipped by the reduce
+    const int Fp = d.Fp;
+    TnPlan p;
+    LdPlain<4> al{dzn, Hp};
+    LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
+    HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, slab, bslab, true, &p, side));
+    HIP_RET(tn_reduce(p, slab, bslab, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
+                      grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F));
+  } else {
     const int vx = vec_for(b->x, F, F);
     TnPlan p;
     hipError_t e = with_vec(vx, [&](auto VX) {
@@ -209,11 +218,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, Hp, Gs, Hp, st));
   }
   if (F > 0) {  // main: dW0[:, :F] = Gs^T x (own slab: runs beside the side stream's work)
-    const int vx = vec_for(b->x, F, F);
+    const float* xb = fv.xp ? fv.xp : b->x;
+    const int64_t ldx = fv.xp ? d.Fp : F;
+    const int vx = vec_for(xb, ldx, F);
     TnPlan p;
     hipError_t e = with_vec(vx, [&](auto VX) {
       LdPlain<4> al{Gs, Hp};
-      LdPlain<decltype(VX)::value> bl{b->x, F};
+      LdPlain<decltype(VX)::value> bl{xb, ldx};
       return tn_gemm("gemm_tn_wgrad_node", al, bl, H, F, N, slab2, bslab2, Fe == 0, &p, st);
     });
     HIP_RET(e);

@@ -79,16 +79,26 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     tj.n = 1;
     HIP_RET(transpose_batch(tj, side));
   }
+  // x rows padded to 16 bytes (F % 4 != 0): the x-GEMM here and both x-part weight gradients
+  // read xp with 16-byte loads
+  const float* xa = b->x;
+  int64_t ldx = F;
+  if (fv.xp) {
+    ProfScope _p("pad_x", side);
+    HIP_RET(pad_rows(b->x, N, F, fv.xp, d.Fp, side));
+    xa = fv.xp;
+    ldx = d.Fp;
+  }
   if (F > 0) {
     ProfScope _p("gemm_nt_x", side);
     int vb = vec_for(W0, F + Fe, F);
     const int vb2 = vec_for(Wn, F + H, F);
     vb = vb < vb2 ? vb : vb2;
-    const int vx = vec_for(b->x, F, F);
+    const int vx = vec_for(xa, ldx, F);
     hipError_t e = with_vec(vx, [&](auto VX) {
       return with_vec(vb, [&](auto VB) {
         return with_nt_rn(2 * H, [&](auto RN) {
-          LdPlain<decltype(VX)::value> al{b->x, F};
+          LdPlain<decltype(VX)::value> al{xa, ldx};
           LdTwoRows<decltype(VB)::value> bl{W0, F + Fe, Wn, F + H, H};
           EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
           return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, 2 * H, F, side);

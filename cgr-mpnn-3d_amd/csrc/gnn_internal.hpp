@@ -65,6 +65,7 @@ struct FloatView {
   float* w0eT;  // [Fe, Hp] transposed edge-feature slice of edge_init.weight
   float* P;     // [N, Hp]  x @ W0[:, :F]^T (node-level half of edge init)
   float* Q;     // [N, Hp]  x @ W_n[:, :F]^T (x-part of the readout, computed beside graph prep)
+  float* xp;    // [N, Fp]  x with rows padded to 4 floats (only when F % 4 != 0; else nullptr)
   float* h[CGR_MAX_DEPTH + 1];    // [E, Hp] h_0 .. h_D
   float* a[CGR_MAX_DEPTH + 1];    // [N, Hp] a_l = scatter_add(h_l, dst); a_D = readout s
   float* pre[CGR_MAX_DEPTH + 1];  // [E, Hp] pre-activations (non-ReLU only; else nullptr)
@@ -75,7 +76,7 @@ struct FloatView {
 
 struct Dims {
   int64_t N, E, B;
-  int F, Fe, Fep, H, Hp, D;
+  int F, Fe, Fep, Fp, H, Hp, D;  // Fp = round_up(F, 4)
   int act;
   int learnable_skip;
 };
@@ -87,7 +88,7 @@ struct ArenaLayout {
   size_t zero_block, zero_bytes, deg_dst, deg_src, cursor, cursor2, graph_cnt, status, rng;
   size_t perm, src_s, dst_s, rev_s, src_list, inv, src_c, dst_c, dst_ptr, src_ptr, graph_ptr,
       node_graph;
-  size_t e_s, w0eT, P, Q, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,
+  size_t e_s, w0eT, P, Q, xp, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,
       g;
 };
 

@@ -1,3 +1,4 @@
+#include <algorithm>
 // Non-GEMM kernels of the D-MPNN path: segmented sums (the sum-scatter of GNN.py:134 / :110),
 // edge init, pooling + ffn head, backward activation kernels, deterministic split-K reduction.
 // All are HBM/L2-streaming kernels: float4 per lane along the hidden dimension, rows of one
@@ -412,6 +413,33 @@ hipError_t edge_init_bwd(const float* dh0, const float* da, const float* dm, con
 }
 
 // ------------------------------------------------------------------------------------------
+// x rows padded to a multiple of 4 floats (F = 846 -> 848): every GEMM that reads x then issues
+// 16-byte loads instead of 8-byte ones
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_pad_rows(const float* __restrict__ x, int64_t N, int F,
+                                                  float* __restrict__ xp, int ldp) {
+  const int c4n = ldp >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * c4n) return;
+  const int64_t r = t / c4n;
+  const int k = 4 * (int)(t - r * c4n);
+  const float* src = x + r * F;
+  float4 v;
+  v.x = k < F ? src[k] : 0.f;
+  v.y = k + 1 < F ? src[k + 1] : 0.f;
+  v.z = k + 2 < F ? src[k + 2] : 0.f;
+  v.w = k + 3 < F ? src[k + 3] : 0.f;
+  *reinterpret_cast<float4*>(xp + r * ldp + k) = v;
+}
+
+hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStream_t st) {
+  const int64_t tot = N * (ldp >> 2);
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pad_rows, dim3(cdiv(tot, 256)), dim3(256), 0, st, x, N, F, xp, ldp);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
 // dropout key (graph-safe: the counter lives on the device and advances per forward)
 // ------------------------------------------------------------------------------------------
 __global__ void k_rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out) {
@@ -432,51 +460,98 @@ hipError_t rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out, hipStrea
 // ------------------------------------------------------------------------------------------
 // deterministic split-K reduction of weight-gradient slabs
 // ------------------------------------------------------------------------------------------
-// slab layout [splits][Nout][ldk], ldk = round_up(Kout, 4) (gemm_tn_kernel): one thread per float4
-// of a slab row, 16-byte loads of every split in a fixed order (deterministic).
-__global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ slab,
-                                                      const float* __restrict__ bslab, int splits,
-                                                      int Nout, int Kout, float* __restrict__ dst,
-                                                      int64_t ld_dst, int64_t col_off,
-                                                      float* __restrict__ bias_dst) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// slab layout [splits][Nout][ldk], ldk = round_up(Kout, 4) (gemm_tn_kernel).  The output is
+// small (a weight matrix) and the split dimension long (up to ~200), so a workgroup owns 32
+// float4 outputs and spreads the splits over 8 thread groups (group g sums splits g, g + 8, ...
+// in order), then combines the 8 partials in a fixed order through LDS: deterministic, and
+// ~40k outputs still give >1000 workgroups.  The bias slabs [splits][Nout] ride along as extra
+// float4-less columns in the last workgroups.
+constexpr int kRedCols = 32, kRedGroups = 8;
+#ifndef CGR_REDUCE_MAX_BLOCKS
+#define CGR_REDUCE_MAX_BLOCKS 256  // A/B: 256 beats 64 and unbounded (4096) by 4-8 %
+#endif
+
+__global__ __launch_bounds__(kRedCols * kRedGroups) void k_reduce_slabs(
+    const float* __restrict__ slab, const float* __restrict__ bslab, int splits, int Nout,
+    int Kout, float* __restrict__ dst, int64_t ld_dst, int64_t col_off, float* __restrict__ bias_dst,
+    int main_blocks, int gap_at, int gap_len) {
+  __shared__ float4 part[kRedGroups][kRedCols];
+  __shared__ float bpart[kRedGroups][kRedCols];
+  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
   const int ldk = (Kout + 3) & ~3;
   const int c4n = ldk >> 2;
   const int64_t nf = (int64_t)Nout * c4n;
-  const int64_t split_f4 = (int64_t)Nout * c4n;  // float4 per split
-  if (t < nf) {
-    const int64_t n = t / c4n;
-    const int k = (int)(t - n * c4n) * 4;
-    const float4* s4 = reinterpret_cast<const float4*>(slab) + t;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll 8
-    for (int p = 0; p < splits; ++p) {
-      const float4 v = s4[(int64_t)p * split_f4];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
+  const int nblk = main_blocks + (bias_dst ? (Nout + kRedCols - 1) / kRedCols : 0);
+  // grid-stride over the logical blocks: the launch is kept narrow (it runs on the side stream
+  // beside the critical path; a wide launch would take every CU's slots from it)
+  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+    if (blk < main_blocks) {
+      const int64_t f = (int64_t)blk * kRedCols + col;
+      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (f < nf) {
+        const float4* s4 = reinterpret_cast<const float4*>(slab) + f;
+#pragma unroll 4
+        for (int p = grp; p < splits; p += kRedGroups) {
+          const float4 v = s4[(int64_t)p * nf];
+          s.x += v.x;
+          s.y += v.y;
+          s.z += v.z;
+          s.w += v.w;
+        }
+      }
+      part[grp][col] = s;
+      __syncthreads();
+      if (grp == 0 && f < nf) {
+        float4 t = part[0][col];
+#pragma unroll
+        for (int g = 1; g < kRedGroups; ++g) {
+          const float4 u = part[g][col];
+          t.x += u.x;
+          t.y += u.y;
+          t.z += u.z;
+          t.w += u.w;
+        }
+        const int64_t n = f / c4n;
+        const int k = (int)(f - n * c4n) * 4;
+        float* o = dst + n * ld_dst + col_off;
+        const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int kk = k + q;
+          if (kk >= Kout || (kk >= gap_at && kk < gap_at + gap_len)) continue;
+          o[kk >= gap_at + gap_len ? kk - gap_len : kk] = tv[q];
+        }
+      }
+    } else {
+      const int64_t n = (int64_t)(blk - main_blocks) * kRedCols + col;
+      float s = 0.f;
+      if (n < Nout)
+        for (int p = grp; p < splits; p += kRedGroups) s += bslab[(int64_t)p * Nout + n];
+      bpart[grp][col] = s;
+      __syncthreads();
+      if (grp == 0 && n < Nout) {
+        float t = bpart[0][col];
+#pragma unroll
+        for (int g = 1; g < kRedGroups; ++g) t += bpart[g][col];
+        bias_dst[n] = t;
+      }
     }
-    float* o = dst + n * ld_dst + col_off + k;
-    o[0] = s.x;
-    if (k + 1 < Kout) o[1] = s.y;
-    if (k + 2 < Kout) o[2] = s.z;
-    if (k + 3 < Kout) o[3] = s.w;
-  } else if (bias_dst && t < nf + Nout) {
-    const int64_t n = t - nf;
-    float s = 0.f;
-    for (int p = 0; p < splits; ++p) s += bslab[(int64_t)p * Nout + n];
-    bias_dst[n] = s;
+    __syncthreads();  // part / bpart reused by the next logical block
   }
 }
 
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
-                        hipStream_t st) {
-  const int64_t tot = (int64_t)Nout * (((Kout + 3) & ~3) >> 2) + (bias_dst ? Nout : 0);
-  if (tot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(tot, 256)), dim3(256), 0, st, slab, bslab, splits,
-                     Nout, Kout, dst, ld_dst, col_off, bias_dst);
+                        hipStream_t st, int gap_at, int gap_len) {
+  const int64_t nf = (int64_t)Nout * (((Kout + 3) & ~3) >> 2);
+  if (gap_len <= 0) gap_at = 0x7fffffff, gap_len = 0;
+  if (nf <= 0) return hipSuccess;
+  const int main_blocks = (int)cdiv(nf, kRedCols);
+  const int bias_blocks = bias_dst ? (int)cdiv(Nout, kRedCols) : 0;
+  const int grid = std::min(main_blocks + bias_blocks, CGR_REDUCE_MAX_BLOCKS);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(grid), dim3(kRedCols * kRedGroups),
+                     0, st, slab, bslab, splits, Nout, Kout, dst, ld_dst, col_off, bias_dst,
+                     main_blocks, gap_at, gap_len);
   return hipGetLastError();
 }
 

@@ -78,9 +78,14 @@ hipError_t edge_init_bwd(const float* dh0, const float* da, const float* dm, con
                          int Hp, int act, float* dpre0, hipStream_t st);
 
 // dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
+// gap_len > 0: slab columns [gap_at, gap_at + gap_len) are padding and skipped; later columns
+// shift down by gap_len in dst (the x | s concat of the readout with x padded to 4 floats)
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
-                        hipStream_t st);
+                        hipStream_t st, int gap_at = 0, int gap_len = 0);
+
+// xp[N, ldp] = x[N, F] with zero padding columns [F, ldp) (16-byte rows for the GEMM loaders)
+hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStream_t st);
 
 // out[j][0] = sum_b part[j * nb + b]   for j < njobs (scalar grads of skip weights)
 struct ScalarReduceJobs {
