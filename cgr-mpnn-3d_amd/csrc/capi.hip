@@ -82,6 +82,7 @@ ArenaLayout arena_layout(const Dims& d) {
   L.P = b.take(4 * N * Hp);
   L.Q = b.take(4 * N * Hp);
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
+  L.wT = b.take(4 * (size_t)(d.D + 1) * d.H * Hp);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
     L.a[l] = l <= d.D ? b.take(4 * N * Hp) : kNone;
@@ -132,6 +133,7 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.P = (float*)at(arena, L.P);
   f.Q = (float*)at(arena, L.Q);
   f.xp = (float*)at(arena, L.xp);
+  f.wT = (float*)at(arena, L.wT);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     f.h[l] = (float*)at(arena, L.h[l]);
     f.a[l] = (float*)at(arena, L.a[l]);
@@ -157,7 +159,6 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.ds = b.take(4 * N * Hp);
   W.Gs = b.take(4 * N * Hp);
   W.dg = b.take(4 * B * Hp);
-  W.wT = b.take(4 * (size_t)(d.D + 1) * d.H * Hp);
   size_t slab = 0, bslab = 0;
   auto acc = [&](int Nout, int Kout, int64_t R) {
     const TnPlan p = tn_plan(Nout, Kout, (int)R);

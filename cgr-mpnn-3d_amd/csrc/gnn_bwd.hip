@@ -66,7 +66,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
   float* ds = reinterpret_cast<float*>(ws + WL.ds);
   float* Gs = reinterpret_cast<float*>(ws + WL.Gs);
-  float* wT = reinterpret_cast<float*>(ws + WL.wT);
+  const float* wT = fv.wT;  // W_l^T, W_n[:, F:]^T, transposed by the forward (side stream)
   float* slab = reinterpret_cast<float*>(ws + WL.slab);
   float* bslab = reinterpret_cast<float*>(ws + WL.bslab);
   float* slab2 = reinterpret_cast<float*>(ws + WL.slab2);
@@ -80,17 +80,6 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   if (!ss) return CGR_ERR_HIP;
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
   hipStream_t side = prof_enabled() ? st : ss->side;
-
-  // transposed weights: wT[l] = W_l^T (l < D), wT[D] = W_n[:, F:]^T, all [H, Hp]
-  {
-    ProfScope _p("weight_transpose", st);
-    TransposeJobs tj{};
-    for (int l = 0; l < D; ++l)
-      tj.job[l] = TransposeJob{params[CGR_PARAM_CONV_W(l)], H, 0, wT + l * HHp, Hp, H, H};
-    tj.job[D] = TransposeJob{params[CGR_PARAM_E2N_W(D)], F + H, F, wT + D * HHp, Hp, H, H};
-    tj.n = D + 1;
-    HIP_RET(transpose_batch(tj, st));
-  }
 
   // head + readout
   {

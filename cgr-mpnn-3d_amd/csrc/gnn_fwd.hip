@@ -71,12 +71,17 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   hipStream_t side = prof_enabled() ? st : ss->side;
   HIP_RET(fork_to(ss, st, side));
 
-  // ---- side stream: edge-feature weight slice + merged x-GEMM ----
-  if (Fe > 0) {
+  // ---- side stream: weight transposes + merged x-GEMM ----
+  {  // W0[:, F:]^T for edge init; W_l^T and W_n[:, F:]^T for the backward (arena)
     ProfScope _p("weight_transpose", side);
+    const int64_t HHp = (int64_t)H * Hp;
     TransposeJobs tj{};
-    tj.job[0] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
-    tj.n = 1;
+    int n = 0;
+    if (Fe > 0) tj.job[n++] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
+    for (int l = 0; l < D; ++l)
+      tj.job[n++] = TransposeJob{params[CGR_PARAM_CONV_W(l)], H, 0, fv.wT + l * HHp, Hp, H, H};
+    tj.job[n++] = TransposeJob{Wn, F + H, F, fv.wT + D * HHp, Hp, H, H};
+    tj.n = n;
     HIP_RET(transpose_batch(tj, side));
   }
   // x rows padded to 16 bytes (F % 4 != 0): the x-GEMM here and both x-part weight gradients

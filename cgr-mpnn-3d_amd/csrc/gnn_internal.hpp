@@ -66,6 +66,8 @@ struct FloatView {
   float* P;     // [N, Hp]  x @ W0[:, :F]^T (node-level half of edge init)
   float* Q;     // [N, Hp]  x @ W_n[:, :F]^T (x-part of the readout, computed beside graph prep)
   float* xp;    // [N, Fp]  x with rows padded to 4 floats (only when F % 4 != 0; else nullptr)
+  float* wT;    // [D+1, H, Hp] W_l^T (l < D) and W_n[:, F:]^T for the backward's NT GEMMs, built
+                // by the forward on its side stream (weights do not change between the two)
   float* h[CGR_MAX_DEPTH + 1];    // [E, Hp] h_0 .. h_D
   float* a[CGR_MAX_DEPTH + 1];    // [N, Hp] a_l = scatter_add(h_l, dst); a_D = readout s
   float* pre[CGR_MAX_DEPTH + 1];  // [E, Hp] pre-activations (non-ReLU only; else nullptr)
@@ -88,13 +90,13 @@ struct ArenaLayout {
   size_t zero_block, zero_bytes, deg_dst, deg_src, cursor, cursor2, graph_cnt, status, rng;
   size_t perm, src_s, dst_s, rev_s, src_list, inv, src_c, dst_c, dst_ptr, src_ptr, graph_ptr,
       node_graph;
-  size_t e_s, w0eT, P, Q, xp, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,
+  size_t e_s, w0eT, P, Q, xp, wT, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,
       g;
 };
 
 struct WorkspaceLayout {
   size_t bytes;
-  size_t dpre[2], dm, dh0, da, dzn, ds, Gs, dg, wT, slab, bslab, slab2, bslab2, dsig_part,
+  size_t dpre[2], dm, dh0, da, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,
       slab_elems, bslab_elems;
   int dsig_blocks;
 };

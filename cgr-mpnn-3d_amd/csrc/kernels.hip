@@ -176,31 +176,56 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
 // ------------------------------------------------------------------------------------------
 // add-pool + ffn head (GNN.py:110): one workgroup per graph
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_pool_head(const float* __restrict__ hn, int Hp,
-                                                   const int* __restrict__ gptr, int H,
-                                                   const float* __restrict__ wf,
-                                                   const float* __restrict__ bf,
-                                                   float* __restrict__ g, float* __restrict__ y) {
+// one workgroup per graph, one thread per float4 column; the node rows of a graph are read 4 at a
+// time (loads issued together, summed in node order)
+constexpr int kPoolThreads = 128;
+
+__global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restrict__ hn, int Hp,
+                                                            const int* __restrict__ gptr, int H,
+                                                            const float* __restrict__ wf,
+                                                            const float* __restrict__ bf,
+                                                            float* __restrict__ g,
+                                                            float* __restrict__ y) {
   const int b = blockIdx.x;
   const int v0 = gptr[b], v1 = gptr[b + 1];
+  const int C4 = Hp >> 2;
   float dot = 0.f;
-  for (int n = threadIdx.x; n < H; n += blockDim.x) {
-    float s = 0.f;
-    for (int v = v0; v < v1; ++v) s += hn[(int64_t)v * Hp + n];
-    g[(int64_t)b * Hp + n] = s;
-    dot += s * wf[n];
+  for (int c = threadIdx.x; c < C4; c += kPoolThreads) {
+    const float* col = hn + 4 * c;
+    float4 s = f4zero();
+    int v = v0;
+    for (; v + 4 <= v1; v += 4) {
+      const float4 x0 = *reinterpret_cast<const float4*>(col + (int64_t)v * Hp);
+      const float4 x1 = *reinterpret_cast<const float4*>(col + (int64_t)(v + 1) * Hp);
+      const float4 x2 = *reinterpret_cast<const float4*>(col + (int64_t)(v + 2) * Hp);
+      const float4 x3 = *reinterpret_cast<const float4*>(col + (int64_t)(v + 3) * Hp);
+      s = f4add(f4add(f4add(f4add(s, x0), x1), x2), x3);
+    }
+    for (; v < v1; ++v) s = f4add(s, *reinterpret_cast<const float4*>(col + (int64_t)v * Hp));
+    *reinterpret_cast<float4*>(g + (int64_t)b * Hp + 4 * c) = s;
+    const int n = 4 * c;
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (n + k < H) dot += sv[k] * wf[n + k];
   }
-  __shared__ float red[4];
+  __shared__ float red[kPoolThreads / 64];
   dot = wave_sum(dot);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dot;
   __syncthreads();
-  if (threadIdx.x == 0) y[b] = (red[0] + red[1]) + (red[2] + red[3]) + bf[0];
+  if (threadIdx.x == 0) {
+    float t = red[0];
+#pragma unroll
+    for (int k = 1; k < kPoolThreads / 64; ++k) t += red[k];
+    y[b] = t + bf[0];
+  }
 }
 
 hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
                          const float* wf, const float* bf, float* g, float* y, hipStream_t st) {
   if (B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pool_head, dim3(B), dim3(256), 0, st, hn, Hp, gptr, H, wf, bf, g, y);
+  hipLaunchKernelGGL(k_pool_head, dim3(B), dim3(kPoolThreads), 0, st, hn, Hp, gptr, H, wf, bf, g,
+                     y);
   return hipGetLastError();
 }
 
