@@ -48,6 +48,9 @@ def parse():
                     help="fused: cgr FusedAdam (one native launch); torch: torch.optim.Adam")
     ap.add_argument("--dropout", type=float, default=0.02,
                     help="dropout p per layer (train.py default 0.02)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL) for the real run; gloo only to rehearse the N>1 code path "
+                         "with several ranks on one GPU")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=10,
@@ -220,11 +223,15 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.graph < 0:
         args.graph = 1 if world == 1 else 0
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ordinal = local % max(1, torch.cuda.device_count())  # == local on a full node
+    torch.cuda.set_device(ordinal)
+    dev = torch.device("cuda", ordinal)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from cgr_mpnn_3D._amd import native
     from cgr_mpnn_3D._amd.ddp import install_grad_allreduce

@@ -18,6 +18,10 @@
 #include "profiling.hpp"
 #include "streams.hpp"
 
+#ifndef CGR_SPLIT_XGEMM
+#define CGR_SPLIT_XGEMM 0
+#endif
+
 namespace cgr {
 
 static void dropout_consts(const float* dropout_p, int training, int l, uint32_t* thresh,
@@ -71,19 +75,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   hipStream_t side = prof_enabled() ? st : ss->side;
   HIP_RET(fork_to(ss, st, side));
 
-  // ---- side stream: weight transposes + merged x-GEMM ----
-  {  // W0[:, F:]^T for edge init; W_l^T and W_n[:, F:]^T for the backward (arena)
-    ProfScope _p("weight_transpose", side);
-    const int64_t HHp = (int64_t)H * Hp;
-    TransposeJobs tj{};
-    int n = 0;
-    if (Fe > 0) tj.job[n++] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
-    for (int l = 0; l < D; ++l)
-      tj.job[n++] = TransposeJob{params[CGR_PARAM_CONV_W(l)], H, 0, fv.wT + l * HHp, Hp, H, H};
-    tj.job[n++] = TransposeJob{Wn, F + H, F, fv.wT + D * HHp, Hp, H, H};
-    tj.n = n;
-    HIP_RET(transpose_batch(tj, side));
-  }
+  // ---- side stream: x padding, edge-feature weight slice, x-GEMM(s), backward transposes ----
   // x rows padded to 16 bytes (F % 4 != 0): the x-GEMM here and both x-part weight gradients
   // read xp with 16-byte loads
   const float* xa = b->x;
@@ -94,27 +86,74 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     xa = fv.xp;
     ldx = d.Fp;
   }
+  if (Fe > 0) {
+    ProfScope _p("weight_transpose", side);
+    TransposeJobs tj{};
+    tj.job[0] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
+    tj.n = 1;
+    HIP_RET(transpose_batch(tj, side));
+  }
+  hipEvent_t p_ready = nullptr;  // P (and, unless split, Q) written
   if (F > 0) {
-    ProfScope _p("gemm_nt_x", side);
     int vb = vec_for(W0, F + Fe, F);
     const int vb2 = vec_for(Wn, F + H, F);
     vb = vb < vb2 ? vb : vb2;
     const int vx = vec_for(xa, ldx, F);
-    hipError_t e = with_vec(vx, [&](auto VX) {
-      return with_vec(vb, [&](auto VB) {
-        return with_nt_rn(2 * H, [&](auto RN) {
-          LdPlain<decltype(VX)::value> al{xa, ldx};
-          LdTwoRows<decltype(VB)::value> bl{W0, F + Fe, Wn, F + H, H};
-          EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
-          return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, 2 * H, F, side);
+#if CGR_SPLIT_XGEMM
+    // P first (edge init waits for it), Q = x W_n[:, :F]^T afterwards beside the layers
+    for (int part = 0; part < 2; ++part) {
+      ProfScope _p("gemm_nt_x", side);
+      const float* Wb = part == 0 ? W0 : Wn;
+      const int64_t ldw = part == 0 ? F + Fe : F + H;
+      const int vw = vec_for(Wb, ldw, F);
+      hipError_t e = with_vec(vx, [&](auto VX) {
+        return with_vec(vw, [&](auto VW) {
+          return with_nt_rn(H, [&](auto RN) {
+            LdPlain<decltype(VX)::value> al{xa, ldx};
+            LdPlain<decltype(VW)::value> bl{Wb, ldw};
+            EpStore ep{part == 0 ? fv.P : fv.Q, Hp, N, H, nullptr};
+            return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, H, F, side);
+          });
         });
       });
-    });
-    HIP_RET(e);
+      HIP_RET(e);
+      if (part == 0) HIP_RET(record_point(ss, side, &p_ready));
+    }
+    (void)vb;
+#else
+    {
+      ProfScope _p("gemm_nt_x", side);
+      hipError_t e = with_vec(vx, [&](auto VX) {
+        return with_vec(vb, [&](auto VB) {
+          return with_nt_rn(2 * H, [&](auto RN) {
+            LdPlain<decltype(VX)::value> al{xa, ldx};
+            LdTwoRows<decltype(VB)::value> bl{W0, F + Fe, Wn, F + H, H};
+            EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
+            return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, 2 * H, F, side);
+          });
+        });
+      });
+      HIP_RET(e);
+    }
+    HIP_RET(record_point(ss, side, &p_ready));
+#endif
   } else {
     HIP_RET(hipMemsetAsync(fv.P, 0, sizeof(float) * (size_t)N * Hp, side));
     HIP_RET(hipMemsetAsync(fv.Q, 0, sizeof(float) * (size_t)N * Hp, side));
+    HIP_RET(record_point(ss, side, &p_ready));
   }
+  {  // W_l^T and W_n[:, F:]^T for the backward's NT GEMMs (arena), off the critical path
+    ProfScope _p("weight_transpose", side);
+    const int64_t HHp = (int64_t)H * Hp;
+    TransposeJobs tj{};
+    for (int l = 0; l < D; ++l)
+      tj.job[l] = TransposeJob{params[CGR_PARAM_CONV_W(l)], H, 0, fv.wT + l * HHp, Hp, H, H};
+    tj.job[D] = TransposeJob{Wn, F + H, F, fv.wT + D * HHp, Hp, H, H};
+    tj.n = D + 1;
+    HIP_RET(transpose_batch(tj, side));
+  }
+  hipEvent_t side_done;
+  HIP_RET(record_point(ss, side, &side_done));
 
   // ---- main stream: graph bookkeeping, then join ----
   {
@@ -124,7 +163,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     int rc = cgr_graph_prep_impl(pa, st);
     if (rc) return rc;
   }
-  HIP_RET(depend(ss, side, st));
+  HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
 
   {
     ProfScope _p("edge_init_fwd", st);
@@ -164,6 +203,9 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     ProfScope _p2("segsum_dst_fwd", st);
     HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
   }
+
+  // join: Q (split x-GEMM) and the backward transposes; the side stream is idle after this
+  HIP_RET(hipStreamWaitEvent(st, side_done, 0));
 
   // readout: hn = act(s W_n[:, F:]^T + Q + b_n), s = a_D
   {

@@ -179,6 +179,13 @@ def test_stress_graphs_vs_oracle(cuda_device):
                     False, cuda_device)
 
 
+def test_node_width_multiple_of_4_vs_oracle(cuda_device):
+    # F = 80 (78 CGR + 2 MACE): x is read in place with 16-byte loads (no padded copy); every
+    # other case has F % 4 != 0 and exercises the padded-x path
+    _oracle_compare(make_batch(10, n_atoms=24, n_bonds=26, n_mace=2, seed=26), 96, 3, "relu",
+                    False, cuda_device)
+
+
 def test_odd_hidden_size_vs_oracle(cuda_device):
     # H not a multiple of 4 (padded rows) and F odd (scalar x loads)
     _oracle_compare(make_batch(6, n_atoms=14, n_bonds=16, n_mace=7, seed=25), 37, 2, "silu", True,

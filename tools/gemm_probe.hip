@@ -140,6 +140,116 @@ __global__ __launch_bounds__(WAVES * 64) void probe(const float* __restrict__ A,
     }
 }
 
+// warp-specialised variant: CW consumer waves (16 rows x BN cols each: LDS reads + MFMA only)
+// and PW producer waves (global loads -> ds_write of the next stage), one barrier per k-step.
+template <int CW, int PW, int RN, int S>
+__global__ __launch_bounds__((CW + PW) * 64) void wsprobe(const float* __restrict__ A,
+                                                          const float* __restrict__ B,
+                                                          float* __restrict__ C, int M, int N,
+                                                          int K, int tiles_n) {
+  constexpr int BM = CW * 16, BN = RN * 16, ACH = BM * 4, BCH = BN * 4, PT = PW * 64;
+  constexpr int APT = (ACH + PT - 1) / PT, BPT = (BCH + PT - 1) / PT;
+  __shared__ float4 lds[S * (ACH + BCH)];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = K / 16;
+  const bool producer = w >= CW;
+  const int pt = tid - CW * 64;
+  const float* ap[APT];
+  int adst[APT];
+  const float* bp[BPT];
+  int bdst[BPT];
+  if (producer) {
+#pragma unroll
+    for (int p = 0; p < APT; ++p) {
+      const int q = pt + p * PT, r = q >> 2, kc = q & 3;
+      const bool in = q < ACH;
+      ap[p] = A + (int64_t)min(m0 + (in ? r : 0), M - 1) * K + kc * 4;
+      adst[p] = in ? r * 4 + (kc ^ lds_swz(r)) : -1;
+    }
+#pragma unroll
+    for (int p = 0; p < BPT; ++p) {
+      const int q = pt + p * PT, r = q >> 2, kc = q & 3;
+      const bool in = q < BCH;
+      bp[p] = B + (int64_t)min(n0 + (in ? r : 0), N - 1) * K + kc * 4;
+      bdst[p] = in ? r * 4 + (kc ^ lds_swz(r)) : -1;
+    }
+  }
+  auto produce = [&](int t) {
+    float4* As = lds + (t % S) * (ACH + BCH);
+    float4* Bs = As + ACH;
+    float4 ra[APT], rb[BPT];
+#pragma unroll
+    for (int p = 0; p < APT; ++p) ra[p] = *reinterpret_cast<const float4*>(ap[p] + t * 16);
+#pragma unroll
+    for (int p = 0; p < BPT; ++p) rb[p] = *reinterpret_cast<const float4*>(bp[p] + t * 16);
+#pragma unroll
+    for (int p = 0; p < APT; ++p)
+      if (adst[p] >= 0) As[adst[p]] = ra[p];
+#pragma unroll
+    for (int p = 0; p < BPT; ++p)
+      if (bdst[p] >= 0) Bs[bdst[p]] = rb[p];
+  };
+  floatx4 acc[RN];
+#pragma unroll
+  for (int j = 0; j < RN; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fg = lane >> 4, sw = fg ^ lds_swz(fr);
+  if (producer) {
+    for (int t = 0; t < S - 1 && t < nk; ++t) produce(t);
+  }
+  __syncthreads();
+  for (int t = 0; t < nk; ++t) {
+    if (producer) {
+      if (t + S - 1 < nk) produce(t + S - 1);
+    } else {
+      const float4* As = lds + (t % S) * (ACH + BCH);
+      const float4* Bs = As + ACH;
+      const float4 a = As[(w * 16 + fr) * 4 + sw];
+      float4 b[RN];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) b[j] = Bs[(j * 16 + fr) * 4 + sw];
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(a, s), f4get(b[j], s), acc[j], 0, 0,
+                                                        0);
+    }
+    __syncthreads();
+  }
+  if (!producer) {
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + w * 16 + fg * 4 + r, col = n0 + j * 16 + fr;
+        if (row < M && col < N) C[(int64_t)row * N + col] = acc[j][r];
+      }
+  }
+}
+
+template <int CW, int PW, int RN, int S>
+static float runws(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t st,
+                   int reps) {
+  const int tm = (M + CW * 16 - 1) / (CW * 16), tn = (N + RN * 16 - 1) / (RN * 16);
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((wsprobe<CW, PW, RN, S>), dim3(tm * tn), dim3((CW + PW) * 64), 0, st, A, B, C,
+                     M, N, K, tn);
+  CK(hipEventRecord(e0, st));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL((wsprobe<CW, PW, RN, S>), dim3(tm * tn), dim3((CW + PW) * 64), 0, st, A, B,
+                       C, M, N, K, tn);
+  CK(hipEventRecord(e1, st));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1000.f / reps;
+}
+
 template <int MODE, int WAVES, int RN, int KT = 1>
 static float run(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t st,
                  int reps) {
@@ -172,12 +282,11 @@ int main() {
   CK(hipStreamCreate(&st));
   const double fl = 2.0 * M * N * K;
   for (int round = 0; round < 3; ++round) {
-    printf("KT=1: full %7.2f no-mfma %7.2f mfma+lds %7.2f mfma-regs %7.2f | KT=2: full %7.2f no-mfma %7.2f mfma+lds %7.2f mfma-regs %7.2f loads+regmfma %7.2f\n",
-           run<0, 4, 5, 1>(A, B, C, M, N, K, st, 20), run<2, 4, 5, 1>(A, B, C, M, N, K, st, 20),
-           run<3, 4, 5, 1>(A, B, C, M, N, K, st, 20), run<5, 4, 5, 1>(A, B, C, M, N, K, st, 20),
-           run<0, 4, 5, 2>(A, B, C, M, N, K, st, 20), run<2, 4, 5, 2>(A, B, C, M, N, K, st, 20),
-           run<3, 4, 5, 2>(A, B, C, M, N, K, st, 20), run<5, 4, 5, 2>(A, B, C, M, N, K, st, 20),
-           run<6, 4, 5, 2>(A, B, C, M, N, K, st, 20));
+    printf("K=416 regular w4: full %7.2f mfma-regs %7.2f | ws c4p4 S2 %7.2f S3 %7.2f | c4p2 S2 %7.2f | c8p4 S2 %7.2f | c4p4 rn5->S4 %7.2f\n",
+           run<0, 4, 5, 1>(A, B, C, M, N, K, st, 20), run<5, 4, 5, 1>(A, B, C, M, N, K, st, 20),
+           runws<4, 4, 5, 2>(A, B, C, M, N, K, st, 20), runws<4, 4, 5, 3>(A, B, C, M, N, K, st, 20),
+           runws<4, 2, 5, 2>(A, B, C, M, N, K, st, 20), runws<8, 4, 5, 2>(A, B, C, M, N, K, st, 20),
+           runws<4, 4, 5, 4>(A, B, C, M, N, K, st, 20));
   }
   (void)fl;
   return 0;
