@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL) for the real run; gloo only to rehearse the N>1 code path "
                          "with several ranks on one GPU")
+    ap.add_argument("--force-dist", type=int, default=0,
+                    help="initialise the process group and the gradient all-reduce even at N=1 "
+                         "(rehearses the collective inside a captured graph on one GPU)")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=10,
@@ -222,12 +225,18 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.graph < 0:
-        args.graph = 1 if world == 1 else 0
+        # N > 1 too: the RCCL all-reduce of the gradient bucket is captured with the step
+        # (rehearsed on one GPU with --force-dist 1); a failed capture falls back to eager
+        args.graph = 1
     ordinal = local % max(1, torch.cuda.device_count())  # == local on a full node
     torch.cuda.set_device(ordinal)
     dev = torch.device("cuda", ordinal)
-    if world > 1:
+    distributed = world > 1 or bool(args.force_dist)
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -248,7 +257,7 @@ def main():
     model = GNN(F_, 14, depth=D, hidden_sizes=[H] * D, dropout_ps=[args.dropout] * D,
                 use_learnable_skip=c["learnable_skip"]).to(dev)
     model.train()
-    if world > 1:
+    if distributed:
         install_grad_allreduce(model)
     if args.optimizer == "fused":
         from cgr_mpnn_3D._amd.optim import FusedAdam
@@ -279,10 +288,16 @@ def main():
             for _ in range(3):
                 step()
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            step()
-        run = g.replay
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+            run = g.replay
+        except Exception as e:  # noqa: BLE001  (report, then time the eager step instead)
+            log(f"[bench] rank {rank}: graph capture failed ({type(e).__name__}: {e}); eager")
+            torch.cuda.synchronize()
+            args.graph = 0
+            run = step
         for _ in range(args.warmup):
             run()
         torch.cuda.synchronize()
@@ -373,7 +388,7 @@ def main():
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

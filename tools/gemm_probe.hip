@@ -281,12 +281,10 @@ int main() {
   hipStream_t st;
   CK(hipStreamCreate(&st));
   const double fl = 2.0 * M * N * K;
-  for (int round = 0; round < 3; ++round) {
-    printf("K=416 regular w4: full %7.2f mfma-regs %7.2f | ws c4p4 S2 %7.2f S3 %7.2f | c4p2 S2 %7.2f | c8p4 S2 %7.2f | c4p4 rn5->S4 %7.2f\n",
-           run<0, 4, 5, 1>(A, B, C, M, N, K, st, 20), run<5, 4, 5, 1>(A, B, C, M, N, K, st, 20),
-           runws<4, 4, 5, 2>(A, B, C, M, N, K, st, 20), runws<4, 4, 5, 3>(A, B, C, M, N, K, st, 20),
-           runws<4, 2, 5, 2>(A, B, C, M, N, K, st, 20), runws<8, 4, 5, 2>(A, B, C, M, N, K, st, 20),
-           runws<4, 4, 5, 4>(A, B, C, M, N, K, st, 20));
+  for (int round = 0; round < 1; ++round) {
+    printf("w4 KT1: mode6 loads+regmfma %7.2f | mode2 no-mfma %7.2f | mode5 mfma-regs %7.2f | ws c4p4 S3 %7.2f\n",
+           run<6, 4, 5, 1>(A, B, C, M, N, K, st, 5), run<2, 4, 5, 1>(A, B, C, M, N, K, st, 5),
+           run<5, 4, 5, 1>(A, B, C, M, N, K, st, 5), runws<4, 4, 5, 3>(A, B, C, M, N, K, st, 5));
   }
   (void)fl;
   return 0;
