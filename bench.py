@@ -226,7 +226,7 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     if args.graph < 0:
         # N > 1 too: the RCCL all-reduce of the gradient bucket is captured with the step
-        # (rehearsed on one GPU with --force-dist 1); a failed capture falls back to eager
+        # (rehearsed on one GPU with --force-dist 1)
         args.graph = 1
     ordinal = local % max(1, torch.cuda.device_count())  # == local on a full node
     torch.cuda.set_device(ordinal)
@@ -281,6 +281,8 @@ def main():
         step()
     torch.cuda.synchronize()
     run = step
+    if args.graph and distributed and args.dist_backend != "nccl":
+        args.graph = 0  # a gloo collective cannot be recorded into a HIP graph (host copies)
     if args.graph:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -288,16 +290,10 @@ def main():
             for _ in range(3):
                 step()
         torch.cuda.current_stream().wait_stream(s)
-        try:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                step()
-            run = g.replay
-        except Exception as e:  # noqa: BLE001  (report, then time the eager step instead)
-            log(f"[bench] rank {rank}: graph capture failed ({type(e).__name__}: {e}); eager")
-            torch.cuda.synchronize()
-            args.graph = 0
-            run = step
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            step()
+        run = g.replay
         for _ in range(args.warmup):
             run()
         torch.cuda.synchronize()

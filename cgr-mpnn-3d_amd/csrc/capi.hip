@@ -269,6 +269,7 @@ int64_t cgr_gnn_arena_offset(const cgr_gnn_config* cfg, int64_t N, int64_t E, in
 }
 
 int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* b, void* arena, void* stream) {
+  clear_stale_hip_error();
   int rc = validate_config(cfg);
   if (rc) return rc;
   rc = validate_batch(cfg, b);
@@ -285,6 +286,7 @@ int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* b, void* arena, v
 int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,
                     const float* dropout_p, uint64_t seed, uint64_t* rng_counter,
                     int32_t training, void* arena, float* y, void* stream) {
+  clear_stale_hip_error();
   int rc = validate_config(cfg);
   if (rc) return rc;
   rc = validate_batch(cfg, b);
@@ -301,6 +303,7 @@ int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params, const
 int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,
                      const float* dropout_p, uint64_t seed, int32_t training, const void* arena,
                      const float* dy, float* const* grads, void* workspace, void* stream) {
+  clear_stale_hip_error();
   int rc = validate_config(cfg);
   if (rc) return rc;
   rc = validate_batch(cfg, b);
@@ -321,6 +324,7 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, cons
 int cgr_segment_sum(const float* values, int64_t ld_values, const int32_t* index,
                     const int32_t* seg_ptr, int64_t num_segments, int64_t width, float* out,
                     int64_t ld_out, void* stream) {
+  clear_stale_hip_error();
   CGR_CHECK(values != nullptr && seg_ptr != nullptr && out != nullptr,
             "cgr_segment_sum: NULL pointer");
   CGR_CHECK(num_segments >= 0 && width >= 0 && ld_values >= width && ld_out >= width,

@@ -93,6 +93,7 @@ int64_t cgr_dmpnn_conv_scratch_bytes(int64_t num_nodes, int64_t num_edges, int64
 int cgr_dmpnn_conv_forward(const int64_t* edge_index, int64_t N, int64_t E, const float* h,
                            int64_t H, const float* weight, const float* bias, float* a_out,
                            float* h_out, void* scratch, void* stream) {
+  clear_stale_hip_error();
   CGR_CHECK(edge_index && h && weight && bias && a_out && h_out && scratch,
             "cgr_dmpnn_conv_forward: NULL pointer");
   CGR_CHECK(N >= 1 && E >= 2 && E % 2 == 0 && H >= 1 && E < (1ll << 30) && N < (1ll << 31),
@@ -133,6 +134,7 @@ int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t N, int64_t E, con
                             int64_t H, const float* weight, const float* grad_a,
                             const float* grad_h_out, float* grad_h, float* grad_weight,
                             float* grad_bias, void* scratch, void* stream) {
+  clear_stale_hip_error();
   (void)edge_index;
   (void)h;
   CGR_CHECK(weight && grad_h && grad_weight && grad_bias && scratch,

@@ -33,6 +33,11 @@ void set_error(const std::string& msg);
 
 constexpr size_t kAlign = 256;
 
+// Every launching entry point starts with this: hipGetLastError() is per thread and sticky, so an
+// error left by an unrelated earlier HIP call (e.g. a caller's aborted stream capture) would
+// otherwise be reported by our first post-launch check as if our launch had failed.
+inline void clear_stale_hip_error() { (void)hipGetLastError(); }
+
 // Index bookkeeping inside the arena (all int32).
 struct IndexView {
   // zero block (memset each call): deg_dst, deg_src, cursor, cursor2, graph_cnt, status

@@ -113,6 +113,7 @@ using namespace cgr;
 extern "C" int cgr_adam_step(const cgr_adam_tensor* tensors, int32_t num_tensors, double lr,
                              double beta1, double beta2, double eps, double weight_decay,
                              int32_t amsgrad, int32_t maximize, void* stream) {
+  clear_stale_hip_error();
   CGR_CHECK(num_tensors >= 0 && (num_tensors == 0 || tensors != nullptr),
             "cgr_adam_step: bad tensor table");
   hipStream_t st = static_cast<hipStream_t>(stream);
