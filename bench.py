@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--force-dist", type=int, default=0,
                     help="initialise the process group and the gradient all-reduce even at N=1 "
                          "(rehearses the collective inside a captured graph on one GPU)")
+    ap.add_argument("--collate-bench", type=int, default=1,
+                    help="also measure on-device collation (SURVEY §8(f) rank 1), N=1 only")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=10,
@@ -169,6 +171,83 @@ def scatter_add_roofline(edge_index, N, H, dev, reps=50):
                      "timing": f"{reps} back-to-back cgr_segment_sum launches between HIP events "
                                f"on the launch stream, E={E} rows x H={H} -> N={N}"}
     return res
+
+
+def collate_measurement(cfgname, dev, store_graphs=4096, reps=50):
+    """§8(f) rank 1: on-device collation (cgr_collate) of one bench-sized batch of random graph
+    ids out of a device-resident store, vs the PyG collation restated in numpy on the host
+    (oracle/collate_numpy.py, the CPU baseline of this leg)."""
+    import numpy as np
+
+    from cgr_mpnn_3D._amd import native
+    from cgr_mpnn_3D._amd.data import GraphStore
+    from cgr_mpnn_3D._amd.synth import CONFIGS, make_batch
+    from oracle import collate_numpy as oc
+
+    c = CONFIGS[cfgname]
+    allb = make_batch(store_graphs, c["n_atoms"], c["n_bonds"], c["n_mace"], seed=4321)
+    store = GraphStore.from_batch(allb, dev)
+    rng = np.random.default_rng(0)
+    ids = rng.integers(0, store_graphs, size=c["num_graphs"])
+    B = ids.size
+    N, E = store.batch_sizes(ids)
+    lib = native.load()
+    gid = torch.from_numpy(ids).to(dev)
+    x = torch.empty((N, store.F), device=dev)
+    ei = torch.empty((2, E), dtype=torch.int64, device=dev)
+    ea = torch.empty((E, store.Fe), device=dev)
+    bt = torch.empty(N, dtype=torch.int64, device=dev)
+    ptr = torch.empty(B + 1, dtype=torch.int64, device=dev)
+    y = torch.empty(B, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def launch():
+        native.check(lib.cgr_collate(
+            native.ptr(gid), B, native.ptr(store.node_ptr), native.ptr(store.edge_ptr),
+            native.ptr(store.x), store.F, native.ptr(store.edge_index),
+            int(store.edge_index.shape[1]), native.ptr(store.edge_attr), store.Fe,
+            native.ptr(store.y), native.ptr(x), native.ptr(ei), E, native.ptr(ea), native.ptr(bt),
+            native.ptr(ptr), native.ptr(y), stream.cuda_stream))
+
+    for _ in range(5):
+        launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        launch()
+    e1.record(stream)
+    e1.synchronize()
+    us = e0.elapsed_time(e1) * 1e3 / reps
+    # algorithmic bytes: read + write of x, edge_attr, edge_index, write batch/ptr/y, read ids/ptrs
+    nbytes = 2.0 * 4 * (N * store.F + E * store.Fe) + 2.0 * 8 * 2 * E + 8.0 * N + 8 * (B + 1) \
+        + 4.0 * B + 8.0 * 3 * B
+    # end-to-end GraphStore.collate (host ids -> device batch, allocation, H2D of the ids)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(20):
+        store.collate(ids)
+    torch.cuda.synchronize()
+    call_us = (time.perf_counter() - t0) / 20 * 1e6
+    # CPU baseline: numpy restatement of Batch.from_data_list for the same ids
+    arrays = (allb.x, allb.edge_index, allb.edge_attr, allb.y, allb.ptr, store.edge_ptr_h)
+    n_cpu, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 2.0:
+        oc.collate(ids, *arrays)
+        n_cpu += 1
+    cpu_s = (time.perf_counter() - t0) / n_cpu
+    return {"kernel": "cgr_collate", "bound": "hbm", "avg_launch_us": round(us, 3),
+            "achieved": round(nbytes / us / 1e3, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_launch": nbytes,
+            "reactions_per_s": round(B / (us * 1e-6), 1),
+            "graphstore_collate_call_us": round(call_us, 1),
+            "cpu_baseline": {"value": round(B / cpu_s, 1), "unit": "reactions/s", "cores": 1,
+                             "kind": "port",
+                             "sample": f"{n_cpu} numpy Batch.from_data_list restatements of "
+                                       f"{B} graphs (oracle/collate_numpy.py), 1 thread"},
+            "store": f"{store_graphs} {cfgname}-shaped reactions resident "
+                     f"({store.x.numel() * 4 / 1e9:.2f} GB of x)",
+            "timing": f"{reps} back-to-back launches between HIP events"}
 
 
 # ------------------------------------------------------------------------------------------------
@@ -357,6 +436,10 @@ def main():
         roof_all = {k: roofline_entry(k, work[k], rep[k][0], rep[k][1], hbm(k))["frac"]
                     for k in cands}
 
+    coll = None
+    if rank == 0 and world == 1 and args.collate_bench:
+        coll = collate_measurement(args.config, dev)
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         log("[bench] timing the CPU baseline (reference op sequence, torch CPU) ...")
@@ -381,6 +464,8 @@ def main():
             "roofline_frac_by_class": roof_all, "kernel_breakdown": breakdown,
             "cpu_baseline": cpu,
         }
+        if coll is not None:
+            out["collate"] = coll
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)

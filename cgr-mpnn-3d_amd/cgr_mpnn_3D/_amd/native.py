@@ -87,6 +87,10 @@ SIGNATURES = [
     ("cgr_adam_step", c_int32,
      [POINTER(CgrAdamTensor), c_int32, c_double, c_double, c_double, c_double, c_double, c_int32,
       c_int32, c_void_p]),
+    ("cgr_collate", c_int32,
+     [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
+      c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+      c_void_p]),
     ("cgr_profile_enable", c_int32, [c_int32]),
     ("cgr_profile_collect", c_int32, []),
     ("cgr_profile_reset", None, []),

@@ -177,6 +177,22 @@ int cgr_adam_step(const cgr_adam_tensor* tensors, int32_t num_tensors, double lr
                   double beta2, double eps, double weight_decay, int32_t amsgrad,
                   int32_t maximize, void* stream);
 
+/* On-device collation (replaces torch_geometric.loader.DataLoader / Batch.from_data_list in
+ * trainer.py:105-118 over the per-reaction Data of ChemDataset.py:81-94).  The store holds every
+ * graph of a dataset collated once on the device: graph g owns node rows [node_ptr[g],
+ * node_ptr[g+1]) of x [*, F] and edges [edge_ptr[g], edge_ptr[g+1]) of edge_index [2,
+ * num_edges_all] (global node ids) / edge_attr [*, Fe]; y [G] may be NULL.  For graph_ids[0..B)
+ * (device) it writes exactly what Batch.from_data_list would: x_out [sum nodes, F], edge_index_out
+ * [2, num_edges_out] re-based to the running node count, edge_attr_out, batch_out [sum nodes]
+ * (= position in graph_ids), ptr_out [B+1], y_out [B].  The caller sizes the outputs (the counts
+ * are known on the host from its copy of node_ptr / edge_ptr).  Bit-exact; one launch. */
+int cgr_collate(const int64_t* graph_ids, int64_t num_ids, const int64_t* node_ptr,
+                const int64_t* edge_ptr, const float* x, int64_t num_node_features,
+                const int64_t* edge_index, int64_t num_edges_all, const float* edge_attr,
+                int64_t num_edge_features, const float* y, float* x_out, int64_t* edge_index_out,
+                int64_t num_edges_out, float* edge_attr_out, int64_t* batch_out, int64_t* ptr_out,
+                float* y_out, void* stream);
+
 /* Instrumentation (no reference counterpart): per-kernel-class device time measured with HIP
  * events recorded on the launch stream around every launch of cgr_gnn_forward/_backward.
  * Off by default; do not enable while capturing a graph.  cgr_profile_collect() waits for the

@@ -1,0 +1,104 @@
+"""On-device collation (cgr_collate / GraphStore) vs the PyG Batch.from_data_list restatement
+(oracle/collate_numpy.py): bit-exact.  Reference: trainer.py:105-118, ChemDataset.py:81-94."""
+
+import numpy as np
+import pytest
+
+from cgr_mpnn_3D._amd.synth import make_batch
+from oracle import collate_numpy as oc
+
+
+def _store_arrays(b):
+    src_graph = b.batch[b.edge_index[0]]
+    ecount = np.bincount(src_graph, minlength=b.num_graphs)
+    edge_ptr = np.concatenate([[0], np.cumsum(ecount)]).astype(np.int64)
+    return b.x, b.edge_index, b.edge_attr, b.y, b.ptr, edge_ptr
+
+
+def test_oracle_identity_selection_reproduces_the_collated_batch():
+    # collating graphs 0..G-1 of a store built from a collated batch gives that batch back
+    b = make_batch(12, n_atoms=9, n_bonds=11, n_mace=3, seed=5, n_atoms_jitter=4)
+    out = oc.collate(np.arange(12), *_store_arrays(b))
+    for k in ("x", "edge_index", "edge_attr", "batch", "ptr", "y"):
+        assert np.array_equal(out[k], getattr(b, k)), k
+
+
+def test_oracle_matches_per_graph_concatenation():
+    b = make_batch(10, n_atoms=7, n_bonds=8, n_mace=0, seed=6, n_atoms_jitter=3)
+    ids = np.array([7, 2, 2, 9, 0])
+    out = oc.collate(ids, *_store_arrays(b))
+    off = 0
+    for pos, g in enumerate(ids):
+        n0, n1 = b.ptr[g], b.ptr[g + 1]
+        assert np.array_equal(out["x"][off:off + n1 - n0], b.x[n0:n1])
+        assert np.all(out["batch"][off:off + n1 - n0] == pos)
+        off += n1 - n0
+    assert out["edge_index"].min() >= 0 and out["edge_index"].max() < off
+    assert out["ptr"][-1] == off
+
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_mace,jitter,fe", [(768, 0, 14), (7, 5, 14), (0, 3, 0), (2, 0, 14)])
+def test_device_collate_bit_exact(n_mace, jitter, fe, cuda_device):
+    from cgr_mpnn_3D._amd.data import GraphStore
+
+    b = make_batch(40, n_atoms=30, n_bonds=30, n_mace=n_mace, seed=7, n_atoms_jitter=jitter)
+    if fe == 0:
+        b.edge_attr = np.zeros((b.edge_attr.shape[0], 0), np.float32)
+    store = GraphStore.from_batch(b, cuda_device)
+    rng = np.random.default_rng(0)
+    for ids in (rng.integers(0, 40, size=25), np.array([39]), np.arange(40)[::-1],
+                np.array([3, 3, 3])):
+        got = store.collate(ids)
+        ref = oc.collate(ids, *_store_arrays(b))
+        assert np.array_equal(got.x.cpu().numpy(), ref["x"])
+        assert np.array_equal(got.edge_index.cpu().numpy(), ref["edge_index"])
+        assert np.array_equal(got.edge_attr.cpu().numpy(), ref["edge_attr"])
+        assert np.array_equal(got.batch.cpu().numpy(), ref["batch"])
+        assert np.array_equal(got.ptr.cpu().numpy(), ref["ptr"])
+        assert np.array_equal(got.y.cpu().numpy(), ref["y"])
+
+
+@pytest.mark.gpu
+def test_device_collate_feeds_the_model_like_host_collation(cuda_device):
+    import torch
+
+    from cgr_mpnn_3D._amd.data import GraphStore
+    from cgr_mpnn_3D._amd.synth import RxnBatch
+    from cgr_mpnn_3D.models.GNN import GNN
+
+    b = make_batch(30, n_mace=16, seed=8)
+    store = GraphStore.from_batch(b, cuda_device)
+    ids = np.array([4, 17, 0, 29, 11])
+    ref = oc.collate(ids, *_store_arrays(b))
+    host = RxnBatch(**ref).to_torch(cuda_device)
+    torch.manual_seed(0)
+    m = GNN(b.x.shape[1], 14, depth=2, hidden_sizes=[48] * 2).to(cuda_device).eval()
+    with torch.no_grad():
+        assert torch.equal(m(store.collate(ids)), m(host))
+
+
+@pytest.mark.gpu
+def test_graph_store_from_data_list(cuda_device):
+    import torch
+
+    from cgr_mpnn_3D._amd.data import GraphStore
+
+    b = make_batch(6, n_atoms=8, n_bonds=9, n_mace=4, seed=9)
+
+    class D:  # PyG Data stand-in (ChemDataset.py:81-94 fields)
+        def __init__(self, g):
+            n0, n1 = b.ptr[g], b.ptr[g + 1]
+            sel = (b.edge_index[0] >= n0) & (b.edge_index[0] < n1)
+            self.x = torch.from_numpy(b.x[n0:n1])
+            self.edge_index = torch.from_numpy(b.edge_index[:, sel] - n0)
+            self.edge_attr = torch.from_numpy(b.edge_attr[sel])
+            self.y = torch.tensor([b.y[g]])
+
+    store = GraphStore.from_data_list([D(g) for g in range(6)], cuda_device)
+    got = store.collate(np.arange(6))
+    assert np.array_equal(got.x.cpu().numpy(), b.x)
+    assert np.array_equal(got.edge_index.cpu().numpy(), b.edge_index)
+    assert np.array_equal(got.y.cpu().numpy(), b.y)
