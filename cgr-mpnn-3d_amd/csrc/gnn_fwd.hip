@@ -21,6 +21,9 @@
 #ifndef CGR_SPLIT_XGEMM
 #define CGR_SPLIT_XGEMM 0
 #endif
+#ifndef CGR_PAD_ON_MAIN
+#define CGR_PAD_ON_MAIN 0
+#endif
 
 namespace cgr {
 
@@ -67,7 +70,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     dropout_consts(dropout_p, training, l, &t, &s);
     any_dropout = any_dropout || t != 0;
   }
-  if (any_dropout) HIP_RET(rng_key(seed, rng_counter, iv.rng, st));
+  // (the key is computed by the first graph-prep kernel, see PrepArgs)
 
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
@@ -80,12 +83,14 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   // read xp with 16-byte loads
   const float* xa = b->x;
   int64_t ldx = F;
+#if !CGR_PAD_ON_MAIN
   if (fv.xp) {
     ProfScope _p("pad_x", side);
     HIP_RET(pad_rows(b->x, N, F, fv.xp, d.Fp, side));
     xa = fv.xp;
     ldx = d.Fp;
   }
+#endif
   if (Fe > 0) {
     ProfScope _p("weight_transpose", side);
     TransposeJobs tj{};
@@ -160,9 +165,20 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     ProfScope _p("graph_prep", st);
     PrepArgs pa{b->edge_index, b->batch, b->graph_ptr, b->edge_attr, d.N, d.E, d.B,
                 d.Fe,          d.Fep,   iv,           fv.e_s};
+    pa.want_key = any_dropout;
+    pa.seed = seed;
+    pa.rng_counter = rng_counter;
     int rc = cgr_graph_prep_impl(pa, st);
     if (rc) return rc;
   }
+#if CGR_PAD_ON_MAIN
+  // the main stream waits for the x-GEMM anyway: pad x for the backward's TN GEMMs here (the
+  // forward x-GEMM reads x in place)
+  if (fv.xp) {
+    ProfScope _p("pad_x", st);
+    HIP_RET(pad_rows(b->x, N, F, fv.xp, d.Fp, st));
+  }
+#endif
   HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
 
   {

@@ -121,6 +121,10 @@ struct PrepArgs {
   int64_t Fe, Fep;
   IndexView idx;
   float* e_s;
+  // dropout key (folded into the first prep kernel): written to idx.rng when want_key
+  bool want_key = false;
+  uint64_t seed = 0;
+  uint64_t* rng_counter = nullptr;
 };
 
 }  // namespace cgr

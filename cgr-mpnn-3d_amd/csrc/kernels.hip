@@ -465,24 +465,6 @@ hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStr
 }
 
 // ------------------------------------------------------------------------------------------
-// dropout key (graph-safe: the counter lives on the device and advances per forward)
-// ------------------------------------------------------------------------------------------
-__global__ void k_rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out) {
-  uint64_t k = seed;
-  if (counter) {
-    const uint64_t c = counter[0];
-    k = seed + 0xD1B54A32D192ED03ull * (c + 1);
-    counter[0] = c + 1;
-  }
-  key_out[0] = k;
-}
-
-hipError_t rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out, hipStream_t st) {
-  hipLaunchKernelGGL(k_rng_key, dim3(1), dim3(1), 0, st, seed, counter, key_out);
-  return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------------
 // deterministic split-K reduction of weight-gradient slabs
 // ------------------------------------------------------------------------------------------
 // slab layout [splits][Nout][ldk], ldk = round_up(Kout, 4) (gemm_tn_kernel).  The output is

@@ -7,9 +7,6 @@
 namespace cgr {
 
 // out[s, :w] = sum_{j in [ptr[s], ptr[s+1])} vals[idx ? idx[j] : j, :w]
-// dropout key of one forward: key = seed (+ a Weyl step per *counter, which is then incremented)
-hipError_t rng_key(uint64_t seed, uint64_t* counter, uint64_t* key_out, hipStream_t st);
-
 hipError_t segment_sum(const float* vals, int64_t ldv, const int* idx, const int* ptr,
                        int64_t nseg, int64_t width, float* out, int64_t ldo, hipStream_t st);
 
