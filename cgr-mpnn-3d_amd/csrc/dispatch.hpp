@@ -37,6 +37,20 @@ inline auto with_nt_rn(int N, F&& f) {
   return f(IC<4>{});
 }
 
+// Edge-row (layer) NT GEMMs: (WAVES, RN).  Default 4 waves x 5 fragments (64 x 80 tiles) when
+// H tiles by 80; CGR_NT_WIDE selects 8 waves x 13 fragments (128 x 208 tiles) for A/B runs.
+#ifndef CGR_NT_WIDE
+#define CGR_NT_WIDE 0
+#endif
+template <class F>
+inline auto with_nt_layer(int N, F&& f) {
+#if CGR_NT_WIDE
+  if (N > 160) return f(IC<8>{}, IC<13>{});
+#endif
+  if (N % 80 == 0) return f(IC<4>{}, IC<5>{});
+  return f(IC<4>{}, IC<4>{});
+}
+
 // TN GEMM: WAVES from the output-row count (= H), RN from the output-column count.
 template <class F>
 inline auto with_tn_shape(int Nout, int Kout, F&& f) {

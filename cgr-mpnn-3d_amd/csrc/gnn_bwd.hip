@@ -171,11 +171,12 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     // main: dm = dpre W_l ; da[v] = sum_{src(e) = v} dm[e]
     {
       ProfScope _p("gemm_nt_layer_bwd", st);
-      hipError_t e = with_nt_rn(H, [&](auto RN) {
+      hipError_t e = with_nt_layer(H, [&](auto WV, auto RN) {
         LdPlain<4> al{dp, Hp};
         LdPlain<4> bl{wT + l * HHp, Hp};
         EpStore ep{dm, Hp, E, H, nullptr};
-        return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H, st);
+        return launch_gemm_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H,
+                                                                            st);
       });
       HIP_RET(e);
     }

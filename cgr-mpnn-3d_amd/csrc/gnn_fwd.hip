@@ -209,9 +209,10 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       ProfScope _p("gemm_nt_layer_fwd", st);
       const int vw = vec_for(Wl, H, H);
       hipError_t e = with_vec(vw, [&](auto VW) {
-        return with_nt_rn(H, [&](auto RN) {
+        return with_nt_layer(H, [&](auto WV, auto RN) {
           LdPlain<decltype(VW)::value> blw{Wl, H};
-          return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, E, H, H, st);
+          return launch_gemm_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, blw, ep, E,
+                                                                              H, H, st);
         });
       });
       HIP_RET(e);

@@ -250,6 +250,75 @@ static float runws(const float* A, const float* B, float* C, int M, int N, int K
   return ms * 1000.f / reps;
 }
 
+// weight-stationary in REGISTERS: wave w of column group cg owns output columns
+// [cg*80 + 16w, +16) and keeps W[those 16 columns][0..K) in 25 float4 = 100 VGPRs; the workgroup
+// streams 16-row A tiles through LDS (double buffered) over a persistent row range.
+template <int KC>  // KC = K / 16 chunks
+__global__ __launch_bounds__(320) void wregprobe(const float* __restrict__ A,
+                                                 const float* __restrict__ B,
+                                                 float* __restrict__ C, int M, int N, int K,
+                                                 int groups) {
+  constexpr int K4 = KC * 4;  // float4 per row
+  __shared__ float4 As[2][16 * K4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int cg = blockIdx.x % 5, rg = blockIdx.x / 5;
+  const int fr = lane & 15, fg = lane >> 4, sw = fg ^ lds_swz(fr);
+  const int n = cg * 80 + w * 16 + fr;
+  float4 breg[KC];
+#pragma unroll
+  for (int c = 0; c < KC; ++c)
+    breg[c] = *reinterpret_cast<const float4*>(B + (int64_t)min(n, N - 1) * K + 16 * c + 4 * fg);
+  const int ntiles = M / 16;
+  auto load = [&](int t, int buf) {
+    for (int q = tid; q < 16 * K4; q += 320) {
+      const int r = q / K4, kc = q - r * K4;  // kc = float4 index along k
+      const float4 v = *reinterpret_cast<const float4*>(A + (int64_t)(t * 16 + r) * K + 4 * kc);
+      As[buf][((kc >> 2) * 16 + r) * 4 + ((kc & 3) ^ lds_swz(r))] = v;
+    }
+  };
+  int t = rg, buf = 0;
+  if (t < ntiles) load(t, 0);
+  __syncthreads();
+  for (; t < ntiles; t += groups) {
+    const int tn = t + groups;
+    if (tn < ntiles) load(tn, buf ^ 1);
+    floatx4 acc = floatx4{0.f, 0.f, 0.f, 0.f};
+    const float4* Ab = As[buf];
+#pragma unroll
+    for (int c = 0; c < KC; ++c) {
+      const float4 a = Ab[(c * 16 + fr) * 4 + sw];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(f4get(a, j), f4get(breg[c], j), acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = t * 16 + fg * 4 + r;
+      if (n < N) C[(int64_t)row * N + n] = acc[r];
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+}
+
+template <int KC>
+static float runwreg(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t st,
+                     int reps, int groups) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  hipLaunchKernelGGL((wregprobe<KC>), dim3(5 * groups), dim3(320), 0, st, A, B, C, M, N, K, groups);
+  CK(hipEventRecord(e0, st));
+  for (int i = 0; i < reps; ++i)
+    hipLaunchKernelGGL((wregprobe<KC>), dim3(5 * groups), dim3(320), 0, st, A, B, C, M, N, K,
+                       groups);
+  CK(hipEventRecord(e1, st));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  return ms * 1000.f / reps;
+}
+
 template <int MODE, int WAVES, int RN, int KT = 1>
 static float run(const float* A, const float* B, float* C, int M, int N, int K, hipStream_t st,
                  int reps) {
@@ -281,10 +350,11 @@ int main() {
   hipStream_t st;
   CK(hipStreamCreate(&st));
   const double fl = 2.0 * M * N * K;
-  for (int round = 0; round < 1; ++round) {
-    printf("w4 KT1: mode6 loads+regmfma %7.2f | mode2 no-mfma %7.2f | mode5 mfma-regs %7.2f | ws c4p4 S3 %7.2f\n",
-           run<6, 4, 5, 1>(A, B, C, M, N, K, st, 5), run<2, 4, 5, 1>(A, B, C, M, N, K, st, 5),
-           run<5, 4, 5, 1>(A, B, C, M, N, K, st, 5), runws<4, 4, 5, 3>(A, B, C, M, N, K, st, 5));
+  for (int round = 0; round < 3; ++round) {
+    printf("K=416 regular w4 full %7.2f | wreg groups 51 %7.2f 102 %7.2f 153 %7.2f 204 %7.2f\n",
+           run<0, 4, 5, 1>(A, B, C, M, N, K, st, 20), runwreg<26>(A, B, C, M, N, K, st, 20, 51),
+           runwreg<26>(A, B, C, M, N, K, st, 20, 102), runwreg<26>(A, B, C, M, N, K, st, 20, 153),
+           runwreg<26>(A, B, C, M, N, K, st, 20, 204));
   }
   (void)fl;
   return 0;
