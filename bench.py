@@ -56,6 +56,8 @@ def parse():
                          "(rehearses the collective inside a captured graph on one GPU)")
     ap.add_argument("--collate-bench", type=int, default=1,
                     help="also measure on-device collation (SURVEY §8(f) rank 1), N=1 only")
+    ap.add_argument("--infer-bench", type=int, default=1,
+                    help="also measure the eval forward (SURVEY §8(f) rank 3), N=1 only")
     ap.add_argument("--cpu-baseline", type=int, default=1)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--profile-steps", type=int, default=10,
@@ -250,6 +252,36 @@ def collate_measurement(cfgname, dev, store_graphs=4096, reps=50):
             "timing": f"{reps} back-to-back launches between HIP events"}
 
 
+def inference_measurement(model, data, B, dev, steps=50):
+    """§8(f) rank 3: eval-mode forward only (dropout off, no autograd) on the bench batch,
+    captured into a HIP graph like the training step; reactions/s."""
+    was = model.training
+    model.eval()
+    try:
+        with torch.no_grad():
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                for _ in range(3):
+                    model(data)
+            torch.cuda.current_stream().wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                model(data)
+            for _ in range(5):
+                g.replay()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                g.replay()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+    finally:
+        model.train(was)
+    return {"metric": "reactions/s (eval forward, batched)", "value": round(B * steps / el, 1),
+            "ms_per_batch": round(el / steps * 1e3, 4), "batch": B, "graph_captured": True}
+
+
 # ------------------------------------------------------------------------------------------------
 def cpu_baseline(cfgname, seconds, dropout):
     """Reference CPU path (oracle/dmpnn_torch.py: the reference ATen op sequence incl. its dead
@@ -439,6 +471,9 @@ def main():
     coll = None
     if rank == 0 and world == 1 and args.collate_bench:
         coll = collate_measurement(args.config, dev)
+    infer = None
+    if rank == 0 and world == 1 and args.infer_bench:
+        infer = inference_measurement(model, data, B, dev)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -466,6 +501,8 @@ def main():
         }
         if coll is not None:
             out["collate"] = coll
+        if infer is not None:
+            out["inference"] = infer
         if cpu:
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)

@@ -160,7 +160,7 @@ int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t N, int64_t E, con
       LdGatherDiff<true> bl{a_p, h_p, src_c, nullptr, Hp};
       const TnPlan p = tn_plan((int)H, (int)H, (int)E);
       hipError_t e = with_tn_shape((int)H, (int)H, [&](auto W, auto RN) {
-        return launch_gemm_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(
+        return launch_tn<decltype(W)::value, decltype(RN)::value>(
             al, bl, p, P<float>(scratch, L.slab), P<float>(scratch, L.bslab), (int)H, (int)H,
             (int)E, true, st);
       });

@@ -6,6 +6,7 @@
 #include <type_traits>
 
 #include "gemm.hpp"
+#include "gemm_tn.hpp"
 
 namespace cgr {
 
@@ -69,10 +70,34 @@ inline auto with_tn_shape(int Nout, int Kout, F&& f) {
 #endif
 constexpr int kTnTargetWorkgroups = CGR_TN_TARGET_WGS;
 
+// TN kernel version: 1 = transposed staging + b128 fragment reads (gemm_tn.hpp; same-box A/B:
+// layer wgrad -6% isolated but the step -4% with it, so off), 0 = e-major
+// image with b32 reads (gemm.hpp)
+#ifndef CGR_TN_V2
+#define CGR_TN_V2 0
+#endif
+
 inline TnPlan tn_plan(int Nout, int Kout, int R) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
-    return plan_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(Nout, Kout, R, kTnTargetWorkgroups);
+#if CGR_TN_V2
+    return plan_tn2<decltype(W)::value, 1, decltype(RN)::value>(Nout, Kout, R,
+                                                                 kTnTargetWorkgroups);
+#else
+    return plan_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(Nout, Kout, R,
+                                                                   kTnTargetWorkgroups);
+#endif
   });
+}
+
+template <int W, int RN, class AL, class BL>
+inline hipError_t launch_tn(const AL& al, const BL& bl, const TnPlan& p, float* slab,
+                            float* bslab, int Nout, int Kout, int R, bool want_bias,
+                            hipStream_t st) {
+#if CGR_TN_V2
+  return launch_gemm_tn2<W, 1, RN>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+#else
+  return launch_gemm_tn<W, 1, RN, 1>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+#endif
 }
 
 }  // namespace cgr

@@ -36,7 +36,7 @@ static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout
   const TnPlan p = *plan;
   ProfScope _p(name, st);
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
-    return launch_gemm_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(al, bl, p, slab, bslab,
+    return launch_tn<decltype(W)::value, decltype(RN)::value>(al, bl, p, slab, bslab,
                                                                          Nout, Kout, R, want_bias,
                                                                          st);
   });

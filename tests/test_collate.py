@@ -102,3 +102,30 @@ def test_graph_store_from_data_list(cuda_device):
     assert np.array_equal(got.x.cpu().numpy(), b.x)
     assert np.array_equal(got.edge_index.cpu().numpy(), b.edge_index)
     assert np.array_equal(got.y.cpu().numpy(), b.y)
+
+
+@pytest.mark.gpu
+def test_batched_predict_equals_per_graph_eval(cuda_device):
+    # §8(f) rank 3: test.py's batch_size-1 loop (batch=None per graph, like the CLI) vs one
+    # batched eval forward over device-collated graphs
+    import torch
+
+    from cgr_mpnn_3D._amd.data import GraphStore
+    from cgr_mpnn_3D._amd.infer import predict
+    from cgr_mpnn_3D._amd.synth import TorchBatch
+    from cgr_mpnn_3D.models.GNN import GNN
+
+    b = make_batch(24, n_atoms=20, n_bonds=22, n_mace=8, seed=10, n_atoms_jitter=6)
+    store = GraphStore.from_batch(b, cuda_device)
+    torch.manual_seed(0)
+    m = GNN(b.x.shape[1], 14, depth=3, hidden_sizes=[64] * 3).to(cuda_device)
+    y_batched = predict(m, store, batch_size=10)
+    assert m.training  # restored
+    m.eval()
+    singles = []
+    with torch.no_grad():
+        for g in range(24):
+            one = store.collate([g])
+            singles.append(m(TorchBatch(one.x, one.edge_index, one.edge_attr, None)))
+    y_single = torch.cat([s.reshape(-1) for s in singles])
+    torch.testing.assert_close(y_batched, y_single, rtol=1e-5, atol=1e-5)
