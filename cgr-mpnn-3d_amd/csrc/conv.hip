@@ -123,7 +123,7 @@ int cgr_dmpnn_conv_forward(const int64_t* edge_index, int64_t N, int64_t E, cons
       LdGatherDiff<true> al{a_p, h_p, src_c, nullptr, Hp};
       LdPlain<decltype(VW)::value> bl{weight, H};
       EpStore ep{h_out, H, (int)E, (int)H, bias};
-      return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, (int)E, (int)H, (int)H, st);
+      return launch_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, (int)E, (int)H, (int)H, st);
     });
   });
   HIP_RET(e);
@@ -176,7 +176,7 @@ int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t N, int64_t E, con
       LdPlain<4> al{dout_p, Hp};
       LdPlain<4> bl{wT, Hp};
       EpStore ep{dm, Hp, (int)E, (int)H, nullptr};
-      return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, (int)E, (int)H, (int)H, st);
+      return launch_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, (int)E, (int)H, (int)H, st);
     });
     HIP_RET(e);
     HIP_RET(segment_sum(dm, Hp, P<int>(scratch, L.src_perm), P<int>(scratch, L.src_ptr), N, Hp, da,

@@ -7,6 +7,7 @@
 
 #include "gemm.hpp"
 #include "gemm_tn.hpp"
+#include "gemm_x3.hpp"
 
 namespace cgr {
 
@@ -77,9 +78,28 @@ constexpr int kTnTargetWorkgroups = CGR_TN_TARGET_WGS;
 #define CGR_TN_V2 0
 #endif
 
+// GEMM arithmetic: 1 = fp32 operands split into bf16 hi + lo, three bf16 MFMAs per product
+// (gemm_x3.hpp); 0 = exact fp32 MFMA (gemm.hpp / gemm_tn.hpp)
+#ifndef CGR_GEMM_X3
+#define CGR_GEMM_X3 0
+#endif
+
+template <int W, int RM, int RN, int KT, class AL, class BL, class EP>
+inline hipError_t launch_nt(const AL& al, const BL& bl, const EP& ep, int M, int N, int K,
+                            hipStream_t st) {
+#if CGR_GEMM_X3
+  return launch_gemm_nt_x3<W, RM, RN>(al, bl, ep, M, N, K, st);
+#else
+  return launch_gemm_nt<W, RM, RN, KT>(al, bl, ep, M, N, K, st);
+#endif
+}
+
 inline TnPlan tn_plan(int Nout, int Kout, int R) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
-#if CGR_TN_V2
+#if CGR_GEMM_X3
+    return plan_tn_x3<decltype(W)::value, 1, decltype(RN)::value>(Nout, Kout, R,
+                                                                   kTnTargetWorkgroups);
+#elif CGR_TN_V2
     return plan_tn2<decltype(W)::value, 1, decltype(RN)::value>(Nout, Kout, R,
                                                                  kTnTargetWorkgroups);
 #else
@@ -93,7 +113,9 @@ template <int W, int RN, class AL, class BL>
 inline hipError_t launch_tn(const AL& al, const BL& bl, const TnPlan& p, float* slab,
                             float* bslab, int Nout, int Kout, int R, bool want_bias,
                             hipStream_t st) {
-#if CGR_TN_V2
+#if CGR_GEMM_X3
+  return launch_gemm_tn_x3<W, 1, RN>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+#elif CGR_TN_V2
   return launch_gemm_tn2<W, 1, RN>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
 #else
   return launch_gemm_tn<W, 1, RN, 1>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);

@@ -94,6 +94,13 @@ struct LdPlain {
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(v, rw.ok, k, K);
   }
+  typedef float Raw1;  // single element k (column-blocked staging of the split-bf16 TN kernel)
+  __device__ __forceinline__ Raw1 fetch1(const Row& rw, int k, int K) const {
+    return rw.p[k < K ? k : 0];
+  }
+  __device__ __forceinline__ float combine1(Raw1 v, const Row& rw, int k, int K) const {
+    return (rw.ok && k < K) ? v : 0.f;
+  }
 };
 
 // B rows of two stacked weight matrices: rows [0, n0) from base0 (ld0), rows [n0, ...) from base1
@@ -120,6 +127,13 @@ struct LdTwoRows {
   }
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(v, rw.ok, k, K);
+  }
+  typedef float Raw1;  // single element k (column-blocked staging of the split-bf16 TN kernel)
+  __device__ __forceinline__ Raw1 fetch1(const Row& rw, int k, int K) const {
+    return rw.p[k < K ? k : 0];
+  }
+  __device__ __forceinline__ float combine1(Raw1 v, const Row& rw, int k, int K) const {
+    return (rw.ok && k < K) ? v : 0.f;
   }
 };
 
@@ -152,6 +166,16 @@ struct LdGatherDiff {
   }
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(f4sub(v.a, v.h), rw.ok, k, K);
+  }
+  struct Raw1 {
+    float a, h;
+  };
+  __device__ __forceinline__ Raw1 fetch1(const Row& rw, int k, int K) const {
+    const int kk = k < K ? k : 0;
+    return Raw1{a[(int64_t)rw.s * ld + kk], h[(int64_t)rw.r * ld + kk]};
+  }
+  __device__ __forceinline__ float combine1(const Raw1& v, const Row& rw, int k, int K) const {
+    return (rw.ok && k < K) ? v.a - v.h : 0.f;
   }
 };
 
@@ -199,6 +223,13 @@ struct LdConcat {
   }
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(v, rw.ok, k, K);
+  }
+  typedef float Raw1;  // single element k (column-blocked staging of the split-bf16 TN kernel)
+  __device__ __forceinline__ Raw1 fetch1(const Row& rw, int k, int K) const {
+    return *(k < F ? rw.px + k : (k < K ? rw.ps + (k - F) : rw.px));
+  }
+  __device__ __forceinline__ float combine1(Raw1 v, const Row& rw, int k, int K) const {
+    return (rw.ok && k < K) ? v : 0.f;
   }
 };
 

@@ -118,7 +118,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dzn, Hp};
       LdPlain<4> bl{wT + D * HHp, Hp};
       EpStore ep{ds, Hp, N, H, nullptr};
-      return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, N, H, H, st);
+      return launch_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, N, H, H, st);
     });
     HIP_RET(e);
   }
@@ -175,7 +175,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         LdPlain<4> al{dp, Hp};
         LdPlain<4> bl{wT + l * HHp, Hp};
         EpStore ep{dm, Hp, E, H, nullptr};
-        return launch_gemm_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H,
+        return launch_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H,
                                                                             st);
       });
       HIP_RET(e);

@@ -117,7 +117,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
             LdPlain<decltype(VX)::value> al{xa, ldx};
             LdPlain<decltype(VW)::value> bl{Wb, ldw};
             EpStore ep{part == 0 ? fv.P : fv.Q, Hp, N, H, nullptr};
-            return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, H, F, side);
+            return launch_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, H, F, side);
           });
         });
       });
@@ -134,7 +134,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
             LdPlain<decltype(VX)::value> al{xa, ldx};
             LdTwoRows<decltype(VB)::value> bl{W0, F + Fe, Wn, F + H, H};
             EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
-            return launch_gemm_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, 2 * H, F, side);
+            return launch_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, 2 * H, F, side);
           });
         });
       });
@@ -211,7 +211,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       hipError_t e = with_vec(vw, [&](auto VW) {
         return with_nt_layer(H, [&](auto WV, auto RN) {
           LdPlain<decltype(VW)::value> blw{Wl, H};
-          return launch_gemm_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, blw, ep, E,
+          return launch_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, blw, ep, E,
                                                                               H, H, st);
         });
       });
@@ -233,7 +233,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       return with_nt_rn(H, [&](auto RN) {
         LdPlain<4> al{fv.a[D], Hp};
         LdPlain<decltype(VW)::value> blw{Wn + F, F + H};
-        return launch_gemm_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, N, H, H, st);
+        return launch_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, N, H, H, st);
       });
     });
     HIP_RET(e);
