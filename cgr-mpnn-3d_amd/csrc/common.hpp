@@ -37,13 +37,26 @@ __device__ __forceinline__ float act_grad(float z, int act) {
 }
 
 // Counter-based dropout RNG: keep(seed, layer, element) is a pure function, so the backward
-// regenerates the mask instead of storing it.  splitmix64 finaliser over a 64-bit counter.
+// regenerates the mask instead of storing it.  32-bit integer hash (Wellons' lowbias32
+// finaliser) of a Weyl sequence over the element index, keyed per (seed, layer): ~10 VALU per
+// element where a splitmix64 finaliser (64-bit multiplies) took ~30 -- the mask is evaluated for
+// all E*H elements in both the layer epilogue and layer_act_bwd.  Bijective in the low 32 index
+// bits for a fixed key; keep fractions and neighbour / cross-layer / cross-seed correlations
+// measured at the 1/sqrt(n) noise floor over 6.1M elements.
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
 __device__ __forceinline__ uint32_t drop_hash(uint64_t seed, uint32_t layer, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1) + (uint64_t(layer) << 56);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return uint32_t(z >> 32);
+  const uint32_t k = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + layer * 0x9E3779B9u));
+  uint32_t x = (uint32_t)idx * 0x9E3779B1u + k;
+  x ^= (uint32_t)(idx >> 32) * 0x85EBCA77u;
+  return mix32(x);
 }
 
 // keep with probability 1-p: hash >= p * 2^32
