@@ -437,7 +437,7 @@ struct TNShape {
   static_assert(ACH % NT == 0, "A chunks per thread must be integral");
 };
 
-template <int WAVES, int RM, int RN, int KT, class AL, class BL>
+template <int WAVES, int RM, int RN, int KT, class AL, class BL, int PF>
 __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
     AL al, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout, int R,
     int rows_per_split, int tiles_k, int want_bias) {
@@ -476,11 +476,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
     be[p] = bin[p] ? q / (BN / 4) : 0;
     bc[p] = bin[p] ? (q % (BN / 4)) * 4 : 0;
   }
-  // rows of the tile to fetch next (computed one tile ahead: index loads have a tile to land)
+  // rows of the next tile to fetch (computed one tile ahead: index loads have a tile to land)
   typename AL::Row arow[APT];
   typename BL::Row brow[BPT];
-  typename AL::Raw ra[APT];
-  typename BL::Raw rb[BPT];
   auto mkrows = [&](int t) {
     const int e0 = e_begin + t * BE;
 #pragma unroll
@@ -488,32 +486,37 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
 #pragma unroll
     for (int p = 0; p < BPT; ++p) brow[p] = bl.row(e0 + be[p], bin[p] ? e_end : 0);
   };
-  typename AL::Row arow_f[APT];
-  typename BL::Row brow_f[BPT];
-  auto fetch = [&]() {
+  // one tile in registers: the rows it was fetched with (for combine) and the raw loads
+  struct Set {
+    typename AL::Row ar[APT];
+    typename BL::Row br[BPT];
+    typename AL::Raw ra[APT];
+    typename BL::Raw rb[BPT];
+  };
+  auto fetch = [&](Set& x) {
 #pragma unroll
     for (int p = 0; p < APT; ++p) {
-      arow_f[p] = arow[p];
-      ra[p] = al.fetch(arow[p], n0 + ac[p], Nout);
+      x.ar[p] = arow[p];
+      x.ra[p] = al.fetch(arow[p], n0 + ac[p], Nout);
     }
 #pragma unroll
     for (int p = 0; p < BPT; ++p) {
-      brow_f[p] = brow[p];
-      rb[p] = bl.fetch(brow[p], k0 + bc[p], Kout);
+      x.br[p] = brow[p];
+      x.rb[p] = bl.fetch(brow[p], k0 + bc[p], Kout);
     }
   };
-  auto sstore = [&](int buf) {
+  auto sstore = [&](const Set& x, int buf) {
     float* Ab = At + buf * BE * SA;
     float* Bb = Bt + buf * BE * SB;
 #pragma unroll
     for (int p = 0; p < APT; ++p)
       *reinterpret_cast<float4*>(&Ab[ae[p] * SA + ac[p]]) =
-          al.combine(ra[p], arow_f[p], n0 + ac[p], Nout);
+          al.combine(x.ra[p], x.ar[p], n0 + ac[p], Nout);
 #pragma unroll
     for (int p = 0; p < BPT; ++p)
       if (bin[p])
         *reinterpret_cast<float4*>(&Bb[be[p] * SB + bc[p]]) =
-            bl.combine(rb[p], brow_f[p], k0 + bc[p], Kout);
+            bl.combine(x.rb[p], x.br[p], k0 + bc[p], Kout);
   };
 
   floatx4 acc[RM][RN];
@@ -523,22 +526,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
     for (int j = 0; j < RN; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;
   const bool do_bias = want_bias && tkk == 0 && tid < BM;
-
-  if (nt > 0) {
-    mkrows(0);
-    fetch();
-    mkrows(1);
-    sstore(0);
-  }
-  __syncthreads();
   const int fr = lane & 15, fg = lane >> 4;
-  for (int t = 0; t < nt; ++t) {
-    const int cur = t & 1;
-    const bool more = t + 1 < nt;
-    if (more) {
-      fetch();        // tile t+1, rows prepared during the previous iteration
-      mkrows(t + 2);  // index loads for tile t+2
-    }
+  auto compute = [&](int cur) {
     const float* Ab = At + cur * BE * SA;
     const float* Bb = Bt + cur * BE * SB;
 #pragma unroll
@@ -559,7 +548,63 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
 #pragma unroll
       for (int e = 0; e < BE; ++e) bsum += Ab[e * SA + tid];
     }
-    if (more) sstore(cur ^ 1);
+  };
+
+  if constexpr (PF == 1) {
+    Set x;
+    if (nt > 0) {
+      mkrows(0);
+      fetch(x);
+      mkrows(1);
+      sstore(x, 0);
+    }
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      const bool more = t + 1 < nt;
+      if (more) {
+        fetch(x);       // tile t+1, rows prepared during the previous iteration
+        mkrows(t + 2);  // index loads for tile t+2
+      }
+      compute(cur);
+      if (more) sstore(x, cur ^ 1);
+      __syncthreads();
+    }
+  } else if (nt > 0) {
+    // prefetch distance 2: tile t+2 is fetched before tile t is computed and written to LDS at
+    // the end of iteration t+1.  Fetches are unconditional (rows past e_end read row 0, masked by
+    // combine), so no branch separates a load from its consumer; register sets alternate by tile
+    // parity (loop unrolled by 2).
+    Set x0, x1;
+    mkrows(0);
+    fetch(x0);
+    mkrows(1);
+    fetch(x1);
+    mkrows(2);
+    sstore(x0, 0);
+    __syncthreads();
+    int t = 0;
+    for (; t + 2 <= nt; t += 2) {
+      fetch(x0);  // tile t+2
+      mkrows(t + 3);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
+      sstore(x1, 1);  // tile t+1 (t + 1 < nt here)
+      __syncthreads();
+      fetch(x1);  // tile t+3
+      mkrows(t + 4);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < nt) sstore(x0, 0);  // tile t+2
+      __syncthreads();
+    }
+    if (t < nt) {
+      compute(0);
+      __syncthreads();
+    }
+  } else {
     __syncthreads();
   }
 
@@ -604,11 +649,14 @@ inline TnPlan plan_tn(int Nout, int Kout, int R, int target_wgs) {
   return p;
 }
 
-template <int WAVES, int RM, int RN, int KT, class AL, class BL>
+#ifndef CGR_TN_PF
+#define CGR_TN_PF 1  // 2: same-box A/B +1% step time (layer wgrad slower, node/readout faster)
+#endif
+template <int WAVES, int RM, int RN, int KT, class AL, class BL, int PF = CGR_TN_PF>
 inline hipError_t launch_gemm_tn(const AL& al, const BL& bl, const TnPlan& p, float* slab,
                                  float* bslab, int Nout, int Kout, int R, bool want_bias,
                                  hipStream_t st) {
-  hipLaunchKernelGGL((gemm_tn_kernel<WAVES, RM, RN, KT, AL, BL>),
+  hipLaunchKernelGGL((gemm_tn_kernel<WAVES, RM, RN, KT, AL, BL, PF>),
                      dim3(p.tiles_n * p.tiles_k * p.splits), dim3(WAVES * 64), 0, st, al, bl, slab,
                      bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
   return hipGetLastError();
