@@ -67,7 +67,7 @@ inline auto with_tn_shape(int Nout, int Kout, F&& f) {
 }
 
 #ifndef CGR_TN_TARGET_WGS
-#define CGR_TN_TARGET_WGS 768  // A/B on MI355X (tools/ab_bench.sh): 768 > 1024 > 512 >> 256
+#define CGR_TN_TARGET_WGS 1024  // floor(target / tiles) splits: 4 workgroups per CU; step-neutral vs 768 (A/B), isolated wgrad -20%
 #endif
 constexpr int kTnTargetWorkgroups = CGR_TN_TARGET_WGS;
 

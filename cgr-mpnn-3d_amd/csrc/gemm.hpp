@@ -638,7 +638,9 @@ inline TnPlan plan_tn(int Nout, int Kout, int R, int target_wgs) {
   p.tiles_n = (Nout + S::BM - 1) / S::BM;
   p.tiles_k = (Kout + S::BN - 1) / S::BN;
   const int tiles = p.tiles_n * p.tiles_k;
-  int splits = (target_wgs + tiles - 1) / tiles;
+  // floor, not ceil: the grid must not exceed the target (a whole number of workgroups per CU);
+  // one workgroup past it puts an extra one on a few CUs, and those CUs set the kernel's time
+  int splits = target_wgs / tiles;
   const int max_splits = (R + 4 * S::BE - 1) / (4 * S::BE);  // >= 4 k-tiles per split
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
