@@ -95,12 +95,14 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("gemm_tn_wgrad_readout", 1, 2.0 * N * H * (F + H),
         f4 * (N * H + N * F + N * H + H * (F + H) + H))
     add("gemm_nt_readout_bwd", 1, 2.0 * N * H * H, f4 * (N * H + H * H + N * H))
-    add("layer_act_bwd", D, 0.0, f4 * (N * H + 5 * E * H) + 2 * i4 * E)
+    add("layer_act_bwd", 1, 0.0, f4 * (N * H + 4 * E * H) + i4 * E)  # top layer: dh = ds[dst]
+    # da = segsum_src(dm) fused with the layer below's activation backward (D - 1 launches) or the
+    # edge-init backward (1): dm once, h_{l+1} mask, dh0 read + write, dpre write (+ indices)
+    add("segsum_act_bwd", D, 2.0 * E * H, f4 * (5 * E * H) + i4 * (2 * E + 2 * (N + 1)))
     add("gemm_tn_wgrad_layer", D, 2.0 * E * H * H,
         f4 * (E * H + N * H + E * H + H * H + H) + 2 * i4 * E)
     add("gemm_nt_layer_bwd", D, 2.0 * E * H * H, f4 * (E * H + H * H + E * H))
-    add("segsum_src_bwd", D + 1, E * H, seg_dst + i4 * E)
-    add("edge_init_bwd", 1, 0.0, f4 * (N * H + 4 * E * H) + 2 * i4 * E)
+    add("segsum_src_bwd", 1, E * H, seg_dst + i4 * E)  # Gs = segsum_src(dpre0) for dW0[:, :F]
     add("gemm_tn_wgrad_edge", 1, 2.0 * E * H * Fe, f4 * (E * H + E * Fe + H * Fe + H))
     add("gemm_tn_wgrad_node", 1, 2.0 * N * H * F, f4 * (N * H + N * F + H * F))
     return w

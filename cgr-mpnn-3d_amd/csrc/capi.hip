@@ -154,7 +154,6 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.dpre[1] = b.take(4 * E * Hp);
   W.dm = b.take(4 * E * Hp);
   W.dh0 = b.take(4 * E * Hp);
-  W.da = b.take(4 * N * Hp);
   W.dzn = b.take(4 * N * Hp);
   W.ds = b.take(4 * N * Hp);
   W.Gs = b.take(4 * N * Hp);
@@ -181,7 +180,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   if (d.F > 0) acc(d.H, d.F, d.N);
   W.slab2 = b.take(4 * (slab > 0 ? slab : 1));
   W.bslab2 = b.take(4 * (bslab > 0 ? bslab : 1));
-  W.dsig_blocks = layer_act_bwd_blocks(d.E, d.Hp);
+  W.dsig_blocks = segsum_act_bwd_blocks(d.E, d.N, d.Hp);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
   W.bytes = b.off;
   return W;

@@ -9,7 +9,8 @@
 //   for l = D-1 .. 0:
 //     dpre = dh_{l+1} * mask * act'(pre_l) ; dh0 += s_l dpre ; ds_l = sum dpre*h0
 //     dW_l = dpre^T (a_l[src] - h_l[rev])  (message recomputed, never stored) ; db_l = colsum
-//     dm = dpre W_l ; da = segsum_src(dm) ; dh_l = da[dst] - dm[rev]
+//     dm = dpre W_l ; da = segsum_src(dm) ; dh_l = da[dst] - dm[rev]  (one fused kernel with the
+//     next lower layer's dpre, da never stored: k_segsum_act_bwd)
 //   dpre0 = (dh0 + dh_0) * act'(pre0)
 //   dW0[:, F:] = dpre0^T e ; db0 = colsum(dpre0) ; dW0[:, :F] = (segsum_src dpre0)^T x
 //
@@ -62,7 +63,6 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
                     reinterpret_cast<float*>(ws + WL.dpre[1])};
   float* dm = reinterpret_cast<float*>(ws + WL.dm);
   float* dh0 = reinterpret_cast<float*>(ws + WL.dh0);
-  float* da = reinterpret_cast<float*>(ws + WL.da);
   float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
   float* ds = reinterpret_cast<float*>(ws + WL.ds);
   float* Gs = reinterpret_cast<float*>(ws + WL.Gs);
@@ -123,17 +123,14 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     HIP_RET(e);
   }
 
-  const int nb = layer_act_bwd_blocks(E, Hp);
-  hipEvent_t tn_done[CGR_MAX_DEPTH];
-  for (int l = D - 1; l >= 0; --l) {
-    float* dp = dpre[l & 1];
-    if (l + 2 <= D - 1) HIP_RET(hipStreamWaitEvent(st, tn_done[l + 2], 0));  // buffer reuse
+  // learnable-skip partial-sum slots per layer (same count for the fused and unfused kernels)
+  const int nb = segsum_act_bwd_blocks(E, N, Hp);
+  auto layer_args = [&](int l) {
     uint32_t thresh;
     float scale;
     dropout_params(dropout_p, training, l, &thresh, &scale);
     LayerBwdArgs la{};
     la.ds = ds;
-    la.da = da;
     la.dm = dm;
     la.dst_s = iv.dst_s;
     la.rev_s = iv.rev_s;
@@ -150,13 +147,20 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.E = E;
     la.H = H;
     la.Hp = Hp;
-    la.dpre = dp;
+    la.dpre = dpre[l & 1];
     la.dh0 = dh0;
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
-    {
-      ProfScope _p("layer_act_bwd", st);
-      HIP_RET(layer_act_bwd(la, nullptr, st));
-    }
+    return la;
+  };
+  hipEvent_t tn_done[CGR_MAX_DEPTH];
+  if (D > 0) {  // top layer: dh_D = ds[dst]
+    ProfScope _p("layer_act_bwd", st);
+    HIP_RET(layer_act_bwd(layer_args(D - 1), nb, st));
+  }
+  // edge init: dpre0 overwrites dh0 in place (each element read then written by one thread)
+  float* dpre0 = dh0;
+  for (int l = D - 1; l >= 0; --l) {
+    float* dp = dpre[l & 1];  // written by the previous iteration's fused kernel (or just above)
     // side: dW_l = dpre^T m_l, db_l = colsum(dpre)
     HIP_RET(fork_to(ss, st, side));
     {
@@ -168,7 +172,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       HIP_RET(tn_reduce(p, slab, bslab, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
                         grads[CGR_PARAM_CONV_B(l)], side));
     }
-    // main: dm = dpre W_l ; da[v] = sum_{src(e) = v} dm[e]
+    // main: dm = dpre W_l
     {
       ProfScope _p("gemm_nt_layer_bwd", st);
       hipError_t e = with_nt_layer(H, [&](auto WV, auto RN) {
@@ -180,18 +184,28 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       });
       HIP_RET(e);
     }
-    {
-      ProfScope _p("segsum_src_bwd", st);
-      HIP_RET(segment_sum(dm, Hp, iv.src_list, iv.src_ptr, N, Hp, da, Hp, st));
+    // main: da[v] = sum_{src(e) = v} dm[e], consumed in place by the layer below:
+    // dh_l = da[dst] - dm[rev] -> dpre_{l-1} (or dpre0 of the edge init when l == 0)
+    ProfScope _p("segsum_act_bwd", st);
+    if (l > 0) {
+      // dpre[(l-1) & 1] was last read by the weight gradient of layer l+1
+      if (l + 1 <= D - 1) HIP_RET(hipStreamWaitEvent(st, tn_done[l + 1], 0));
+      HIP_RET(segsum_act_bwd(layer_args(l - 1), iv.src_list, iv.src_ptr, iv.dst_ptr, N, false,
+                             st));
+    } else {
+      LayerBwdArgs le{};
+      le.dm = dm;
+      le.rev_s = iv.rev_s;
+      le.h0 = fv.h[0];
+      le.pre = fv.pre[0];
+      le.act = d.act;
+      le.E = E;
+      le.H = H;
+      le.Hp = Hp;
+      le.dh0 = dh0;
+      le.dpre = dpre0;
+      HIP_RET(segsum_act_bwd(le, iv.src_list, iv.src_ptr, iv.dst_ptr, N, true, st));
     }
-  }
-
-  // edge init: dpre0 overwrites dh0 in place (each element read then written by one thread)
-  float* dpre0 = dh0;
-  {
-    ProfScope _p("edge_init_bwd", st);
-    HIP_RET(edge_init_bwd(dh0, da, dm, iv.dst_s, iv.rev_s, fv.h[0], fv.pre[0], E, H, Hp, d.act,
-                          dpre0, st));
   }
   float* gW0 = grads[CGR_PARAM_EDGE_INIT_W];
   float* gb0 = grads[CGR_PARAM_EDGE_INIT_B];

@@ -101,7 +101,7 @@ struct ArenaLayout {
 
 struct WorkspaceLayout {
   size_t bytes;
-  size_t dpre[2], dm, dh0, da, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,
+  size_t dpre[2], dm, dh0, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,
       slab_elems, bslab_elems;
   int dsig_blocks;
 };

@@ -328,112 +328,167 @@ hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_gra
 // ------------------------------------------------------------------------------------------
 int layer_act_bwd_blocks(int64_t E, int Hp) { return (int)cdiv(E * (Hp / 4), 256); }
 
+// one float4 of one edge row of the layer backward, given dh = dL/dh_{l+1}[i, n..n+3]:
+// dpre = dh * keep/(1-p) * act'(pre) ; dh0 (+)= sigma * dpre ; dsig += dpre . h0
+__device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
+                                              uint64_t key, float& dsig) {
+  const int64_t o = i * a.Hp + n;
+  float d[4] = {dh.x, dh.y, dh.z, dh.w};
+  if (a.act == ACT_RELU) {  // h_{l+1} > 0 <=> relu active and kept by dropout
+    const float4 hv = *reinterpret_cast<const float4*>(a.hnext + o);
+    const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
+  } else {
+    const float4 zv = *reinterpret_cast<const float4*>(a.pre + o);
+    const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float m = a.scale;
+      if (a.thresh && n + k < a.H)
+        m = drop_keep(key, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
+                                                                                      : 0.f;
+      d[k] = d[k] * m * act_grad(zz[k], a.act);
+    }
+  }
+  const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
+  *reinterpret_cast<float4*>(a.dpre + o) = dp;
+  const float sg = a.sigma ? a.sigma[0] : 1.f;
+  float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
+  acc.x += sg * dp.x;
+  acc.y += sg * dp.y;
+  acc.z += sg * dp.z;
+  acc.w += sg * dp.w;
+  *reinterpret_cast<float4*>(a.dh0 + o) = acc;
+  if (a.dsig_part) {
+    const float4 h0 = *reinterpret_cast<const float4*>(a.h0 + o);
+    const float hz[4] = {h0.x, h0.y, h0.z, h0.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (n + k < a.H) dsig += d[k] * hz[k];
+  }
+}
+
+// one float4 of one edge row of the edge-init backward (GNN.py:85-87 reversed), in place over dh0:
+// dpre0 = (dh0 + dh_1) * act'(pre0)
+__device__ __forceinline__ void edge_init_bwd_row(const LayerBwdArgs& a, int64_t i, int n,
+                                                  float4 dh) {
+  const int64_t o = i * a.Hp + n;
+  float4 d = f4add(*reinterpret_cast<const float4*>(a.dh0 + o), dh);
+  if (a.act == ACT_RELU) {
+    const float4 h = *reinterpret_cast<const float4*>(a.h0 + o);
+    d.x = h.x > 0.f ? d.x : 0.f;
+    d.y = h.y > 0.f ? d.y : 0.f;
+    d.z = h.z > 0.f ? d.z : 0.f;
+    d.w = h.w > 0.f ? d.w : 0.f;
+  } else {
+    const float4 z = *reinterpret_cast<const float4*>(a.pre + o);
+    d.x *= act_grad(z.x, a.act);
+    d.y *= act_grad(z.y, a.act);
+    d.z *= act_grad(z.z, a.act);
+    d.w *= act_grad(z.w, a.act);
+  }
+  *reinterpret_cast<float4*>(a.dpre + o) = d;
+}
+
+__device__ __forceinline__ void block_partial(float v, float* dst) {
+  __shared__ float red[4];
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) dst[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 __global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
   const int C4 = a.Hp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float dsig = 0.f;
   if (t < a.E * C4) {
     const int64_t i = t / C4;
-    const int c = (int)(t - i * C4);
-    const int n = 4 * c;
-    const int64_t o = i * a.Hp + n;
-    float4 dh;
-    if (a.first) {
-      dh = *reinterpret_cast<const float4*>(a.ds + (int64_t)a.dst_s[i] * a.Hp + n);
-    } else {
-      dh = f4sub(*reinterpret_cast<const float4*>(a.da + (int64_t)a.dst_s[i] * a.Hp + n),
-                 *reinterpret_cast<const float4*>(a.dm + (int64_t)a.rev_s[i] * a.Hp + n));
-    }
-    float d[4] = {dh.x, dh.y, dh.z, dh.w};
-    const uint64_t key = a.thresh ? *a.seed : 0;
-    if (a.act == ACT_RELU) {
-      const float4 hv = *reinterpret_cast<const float4*>(a.hnext + o);
-      const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
-    } else {
-      const float4 zv = *reinterpret_cast<const float4*>(a.pre + o);
-      const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float m = a.scale;
-        if (a.thresh && n + k < a.H)
-          m = drop_keep(key, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
-                                                                                        : 0.f;
-        d[k] = d[k] * m * act_grad(zz[k], a.act);
-      }
-    }
-    const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
-    *reinterpret_cast<float4*>(a.dpre + o) = dp;
-    const float sg = a.sigma ? a.sigma[0] : 1.f;
-    float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
-    acc.x += sg * dp.x;
-    acc.y += sg * dp.y;
-    acc.z += sg * dp.z;
-    acc.w += sg * dp.w;
-    *reinterpret_cast<float4*>(a.dh0 + o) = acc;
-    if (a.dsig_part) {
-      const float4 h0 = *reinterpret_cast<const float4*>(a.h0 + o);
-      const float hz[4] = {h0.x, h0.y, h0.z, h0.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        if (n + k < a.H) dsig += d[k] * hz[k];
-    }
+    const int n = 4 * (int)(t - i * C4);
+    // top layer: dh_D[i] = ds[dst(i)] (lower layers: k_segsum_act_bwd)
+    const float4 dh = *reinterpret_cast<const float4*>(a.ds + (int64_t)a.dst_s[i] * a.Hp + n);
+    layer_bwd_row(a, i, n, dh, a.thresh ? *a.seed : 0, dsig);
   }
-  if (a.dsig_part) {
-    __shared__ float red[4];
-    dsig = wave_sum(dsig);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = dsig;
-    __syncthreads();
-    if (threadIdx.x == 0) a.dsig_part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-  }
+  if (a.dsig_part) block_partial(dsig, a.dsig_part);
 }
 
-hipError_t layer_act_bwd(const LayerBwdArgs& a, int* nblocks_out, hipStream_t st) {
-  const int nb = layer_act_bwd_blocks(a.E, a.Hp);
-  if (nblocks_out) *nblocks_out = nb;
-  if (nb <= 0) return hipSuccess;
+hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st) {
+  const int need = layer_act_bwd_blocks(a.E, a.Hp);
+  const int nb = nblocks > need ? nblocks : need;  // extra blocks write zero partials
+  if (need <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_layer_bwd, dim3(nb), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_edge_init_bwd(
-    const float* __restrict__ dh0, const float* __restrict__ da, const float* __restrict__ dm,
-    const int* __restrict__ dst_s, const int* __restrict__ rev_s, const float* __restrict__ h0,
-    const float* __restrict__ pre0, int64_t E, int Hp, int act, float* __restrict__ dpre0) {
-  const int C4 = Hp >> 2;
+// src segmented sum of dm fused with the consumer of its result (the next lower layer's
+// activation backward, or the edge-init backward).  Thread (v, float4 column c):
+//   da[v] = sum_{src(e) = v} dm[e]       (rows gathered through src_list, the same row order and
+//                                         float4 adds as k_segsum_v4<true>: bitwise the unfused da)
+//   for every edge i with dst(i) = v (contiguous in dst order):  dh = da[v] - dm[rev(i)], then
+//   layer_bwd_row / edge_init_bwd_row of row i.
+// da never reaches memory (the unfused pair wrote it and read it back gathered per edge).  The
+// grid is a.nblocks blocks (>= the threads needed) so the learnable-skip partial sums fill
+// exactly the slots the unfused kernel fills.
+template <bool EDGE_INIT>
+__global__ __launch_bounds__(256) void k_segsum_act_bwd(LayerBwdArgs a, const int* __restrict__ src_list,
+                                                        const int* __restrict__ src_ptr,
+                                                        const int* __restrict__ dst_ptr, int64_t N) {
+  const int C4 = a.Hp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= E * C4) return;
-  const int64_t i = t / C4;
-  const int n = 4 * (int)(t - i * C4);
-  const int64_t o = i * Hp + n;
-  float4 d = f4add(*reinterpret_cast<const float4*>(dh0 + o),
-                   f4sub(*reinterpret_cast<const float4*>(da + (int64_t)dst_s[i] * Hp + n),
-                         *reinterpret_cast<const float4*>(dm + (int64_t)rev_s[i] * Hp + n)));
-  if (act == ACT_RELU) {
-    const float4 h = *reinterpret_cast<const float4*>(h0 + o);
-    d.x = h.x > 0.f ? d.x : 0.f;
-    d.y = h.y > 0.f ? d.y : 0.f;
-    d.z = h.z > 0.f ? d.z : 0.f;
-    d.w = h.w > 0.f ? d.w : 0.f;
-  } else {
-    const float4 z = *reinterpret_cast<const float4*>(pre0 + o);
-    d.x *= act_grad(z.x, act);
-    d.y *= act_grad(z.y, act);
-    d.z *= act_grad(z.z, act);
-    d.w *= act_grad(z.w, act);
+  float dsig = 0.f;
+  if (t < N * C4) {
+    const int64_t v = t / C4;
+    const int n = 4 * (int)(t - v * C4);
+    const float* base = a.dm + n;
+    auto ld4 = [&](int64_t r) { return *reinterpret_cast<const float4*>(base + r * a.Hp); };
+    const int b = src_ptr[v], e = src_ptr[v + 1];
+    float4 da = f4zero();
+    int j = b;
+    for (; j + 4 <= e; j += 4) {
+      const int64_t r0 = src_list[j], r1 = src_list[j + 1], r2 = src_list[j + 2],
+                    r3 = src_list[j + 3];
+      const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2), x3 = ld4(r3);
+      da = f4add(f4add(f4add(f4add(da, x0), x1), x2), x3);
+    }
+    const int rem = e - j;
+    if (rem > 0) {
+      const int64_t r0 = src_list[j], r1 = src_list[min(j + 1, e - 1)],
+                    r2 = src_list[min(j + 2, e - 1)];
+      const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2);
+      da = f4add(da, x0);
+      if (rem > 1) da = f4add(da, x1);
+      if (rem > 2) da = f4add(da, x2);
+    }
+    const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
+    const int ib = dst_ptr[v], ie = dst_ptr[v + 1];
+    for (int i = ib; i < ie; ++i) {
+      const float4 dh = f4sub(da, ld4(a.rev_s[i]));
+      if constexpr (EDGE_INIT)
+        edge_init_bwd_row(a, i, n, dh);
+      else
+        layer_bwd_row(a, i, n, dh, key, dsig);
+    }
   }
-  *reinterpret_cast<float4*>(dpre0 + o) = d;
+  if (!EDGE_INIT && a.dsig_part) block_partial(dsig, a.dsig_part);
 }
 
-hipError_t edge_init_bwd(const float* dh0, const float* da, const float* dm, const int* dst_s,
-                         const int* rev_s, const float* h0, const float* pre0, int64_t E, int H,
-                         int Hp, int act, float* dpre0, hipStream_t st) {
-  (void)H;
-  if (E <= 0) return hipSuccess;
-  const int64_t tot = E * (Hp / 4);
-  hipLaunchKernelGGL(k_edge_init_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dh0, da, dm, dst_s,
-                     rev_s, h0, pre0, E, Hp, act, dpre0);
+int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp) {
+  return (int)cdiv((E > N ? E : N) * (Hp / 4), 256);
+}
+
+hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int* src_ptr,
+                          const int* dst_ptr, int64_t N, bool edge_init, hipStream_t st) {
+  if (N <= 0 || a.Hp % 4) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
+  // as many blocks as the unfused layer kernel when learnable-skip partials are written
+  const int nb = (!edge_init && a.dsig_part) ? segsum_act_bwd_blocks(a.E, N, a.Hp)
+                                             : (int)cdiv(N * (a.Hp / 4), 256);
+  if (edge_init)
+    hipLaunchKernelGGL(k_segsum_act_bwd<true>, dim3(nb), dim3(256), 0, st, a, src_list, src_ptr,
+                       dst_ptr, N);
+  else
+    hipLaunchKernelGGL(k_segsum_act_bwd<false>, dim3(nb), dim3(256), 0, st, a, src_list,
+                       src_ptr, dst_ptr, N);
   return hipGetLastError();
 }
 

@@ -44,9 +44,9 @@ hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_gra
                            float* dzn, hipStream_t st);
 
 struct LayerBwdArgs {
-  // dh_{l+1}: first layer (l == D-1): ds[dst_s[i]], else da[dst_s[i]] - dm[rev_s[i]]
+  // dh_{l+1}: top layer (l == D-1, layer_act_bwd): ds[dst_s[i]]; below (segsum_act_bwd):
+  // da[dst(i)] - dm[rev_s[i]] with da = segsum_src(dm) computed in the same kernel
   const float* ds;
-  const float* da;
   const float* dm;
   const int* dst_s;
   const int* rev_s;
@@ -66,14 +66,18 @@ struct LayerBwdArgs {
   float* dh0;         // written (first) or accumulated
   float* dsig_part;   // [gridDim] partial sums of dpre*h0 (nullable)
 };
-hipError_t layer_act_bwd(const LayerBwdArgs& a, int* nblocks_out, hipStream_t st);
+// nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
+hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);
 int layer_act_bwd_blocks(int64_t E, int Hp);
+// da = segsum_src(dm) (never stored) fused with the layer backward of every edge row i whose
+// dst is the segment's node (dh = da[dst(i)] - dm[rev(i)]), or with the edge-init backward
+// (edge_init: a.dh0 -> a.dpre in place, a.h0 / a.pre = h_0 / pre_0).  With learnable-skip
+// partials it launches segsum_act_bwd_blocks(E, N, Hp) blocks (size dsig_part accordingly).
+hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int* src_ptr,
+                          const int* dst_ptr, int64_t N, bool edge_init, hipStream_t st);
+int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp);
 
 // dpre0 = (dh0 + da[dst_s] - dm[rev_s]) * act'(pre0)   (ReLU: h0 > 0)
-hipError_t edge_init_bwd(const float* dh0, const float* da, const float* dm, const int* dst_s,
-                         const int* rev_s, const float* h0, const float* pre0, int64_t E, int H,
-                         int Hp, int act, float* dpre0, hipStream_t st);
-
 // dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
 // gap_len > 0: slab columns [gap_at, gap_at + gap_len) are padding and skipped; later columns
 // shift down by gap_len in dst (the x | s concat of the readout with x padded to 4 floats)

@@ -45,9 +45,11 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
             return "gemm_nt_readout_fwd"
         if "EpStore" in n:  # dm = dpre W (E rows) vs ds = dzn W_n (N rows): larger grid is E
             return "gemm_nt_layer_bwd" if grid == max(grids_by_name[n]) else "gemm_nt_readout_bwd"
+    if "k_segsum_act_bwd" in n:
+        return "segsum_act_bwd"
     if "k_segsum" in n:
         return "segsum_src_bwd" if "<true>" in n else "segsum_dst_fwd"
-    table = {"k_edge_init_bwd": "edge_init_bwd", "k_edge_init": "edge_init_fwd",
+    table = {"k_edge_init": "edge_init_fwd",
              "k_layer_bwd": "layer_act_bwd", "k_pool_head": "pool_head_fwd",
              "k_head_bwd": "head_readout_bwd", "k_readout_bwd": "head_readout_bwd",
              "k_reduce_slabs": "splitk_reduce"}
