@@ -84,6 +84,9 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("gemm_nt_x", 1, 2.0 * N * F * 2 * H, f4 * (N * F + 2 * H * F + 2 * N * H))
     add("edge_init_fwd", 1, 2.0 * E * Fe * H,
         f4 * (N * H + E * Fe + Fe * H + H + E * H * (1 + pre)) + i4 * E)
+    # edge init fused with a_0 = segsum_dst(h0) (H <= 512)
+    add("edge_init_seg_fwd", 1, 2.0 * E * Fe * H + E * H,
+        f4 * (N * H + E * Fe + Fe * H + H + E * H * (1 + pre) + N * H) + i4 * (E + N + 1))
     seg_dst = f4 * (E * H + N * H) + i4 * (N + 1)
     add("segsum_dst_fwd", D + 1, E * H, seg_dst)
     add("gemm_nt_layer_fwd", D, 2.0 * E * H * H,

@@ -181,12 +181,16 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
 #endif
   HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
 
-  {
-    ProfScope _p("edge_init_fwd", st);
-    HIP_RET(edge_init_fwd(fv.P, iv.src_s, fv.e_s, Fe, d.Fep, fv.w0eT, b0, E, H, Hp, d.act,
-                          fv.h[0], fv.pre[0], st));
-  }
-  {
+  if (Hp <= 512) {  // edge init + a_0 in one pass
+    ProfScope _p("edge_init_seg_fwd", st);
+    HIP_RET(edge_init_segsum_fwd(fv.P, iv.src_s, fv.e_s, Fe, d.Fep, fv.w0eT, b0, iv.dst_ptr, N,
+                                 H, Hp, d.act, fv.h[0], fv.pre[0], fv.a[0], st));
+  } else {
+    {
+      ProfScope _p("edge_init_fwd", st);
+      HIP_RET(edge_init_fwd(fv.P, iv.src_s, fv.e_s, Fe, d.Fep, fv.w0eT, b0, E, H, Hp, d.act,
+                            fv.h[0], fv.pre[0], st));
+    }
     ProfScope _p("segsum_dst_fwd", st);
     HIP_RET(segment_sum(fv.h[0], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[0], Hp, st));
   }

@@ -173,6 +173,102 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
   return hipGetLastError();
 }
 
+// Edge init fused with the first dst segmented sum: a_0[v] = sum_{dst(i) = v} h0[i].  A block
+// owns kEiNodes consecutive nodes, i.e. the contiguous dst-sorted edge range of their in-edges;
+// thread c owns float4 column c, keeps its slice of W0[:, F:]^T (Fe x 4) in registers across
+// all those edges (the per-edge kernel reloaded it for every edge: 14 float4 + 14 scalar loads
+// per output float4), and sums its edges' h0 into a_0 in edge order -- the same adds, in the same
+// order, as k_edge_init followed by k_segsum_v4<false>, so h0 / pre0 / a_0 are bitwise unchanged.
+constexpr int kEiNodes = 4;
+constexpr int kEiMaxFe = 16;
+
+template <bool REG>
+__global__ __launch_bounds__(128) void k_edge_init_seg(
+    const float* __restrict__ P, const int* __restrict__ src_s, const float* __restrict__ e_s,
+    int Fe, int Fep, const float* __restrict__ w0eT, const float* __restrict__ b0,
+    const int* __restrict__ dst_ptr, int64_t N, int H, int Hp, int act, float* __restrict__ h0,
+    float* __restrict__ pre0, float* __restrict__ a) {
+  const int C4 = Hp >> 2;
+  const int c = threadIdx.x;
+  if (c >= C4) return;  // no barriers below
+  const int n = 4 * c;
+  const float4 bias = make_float4(b0[min(n, H - 1)], b0[min(n + 1, H - 1)],
+                                  b0[min(n + 2, H - 1)], b0[min(n + 3, H - 1)]);
+  float4 w[REG ? kEiMaxFe : 1];
+  if constexpr (REG) {
+#pragma unroll
+    for (int q = 0; q < kEiMaxFe; ++q)
+      w[q] = q < Fe ? *reinterpret_cast<const float4*>(w0eT + (int64_t)q * Hp + n) : f4zero();
+  }
+  const int64_t v0 = (int64_t)blockIdx.x * kEiNodes;
+  const int64_t v1 = v0 + kEiNodes < N ? v0 + kEiNodes : N;
+  for (int64_t v = v0; v < v1; ++v) {
+    float4 acc = f4zero();
+    const int ie = dst_ptr[v + 1];
+    for (int i = dst_ptr[v]; i < ie; ++i) {
+      float4 z = *reinterpret_cast<const float4*>(P + (int64_t)src_s[i] * Hp + n);
+      z.x += bias.x;
+      z.y += bias.y;
+      z.z += bias.z;
+      z.w += bias.w;
+      const float* er = e_s + (int64_t)i * Fep;
+      if constexpr (REG) {
+#pragma unroll
+        for (int q4 = 0; q4 < kEiMaxFe / 4; ++q4) {
+          if (4 * q4 >= Fe) break;
+          const float4 ev = *reinterpret_cast<const float4*>(er + 4 * q4);
+          const float e4[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            if (4 * q4 + k >= Fe) break;
+            const float4 wq = w[4 * q4 + k];
+            z.x += e4[k] * wq.x;
+            z.y += e4[k] * wq.y;
+            z.z += e4[k] * wq.z;
+            z.w += e4[k] * wq.w;
+          }
+        }
+      } else {
+        for (int q = 0; q < Fe; ++q) {
+          const float ev = er[q];
+          const float4 wq = *reinterpret_cast<const float4*>(w0eT + (int64_t)q * Hp + n);
+          z.x += ev * wq.x;
+          z.y += ev * wq.y;
+          z.z += ev * wq.z;
+          z.w += ev * wq.w;
+        }
+      }
+      const int64_t o = (int64_t)i * Hp + n;
+      if (pre0) *reinterpret_cast<float4*>(pre0 + o) = z;
+      float4 h;
+      h.x = act_fwd(z.x, act);
+      h.y = act_fwd(z.y, act);
+      h.z = act_fwd(z.z, act);
+      h.w = act_fwd(z.w, act);
+      *reinterpret_cast<float4*>(h0 + o) = h;
+      acc = f4add(acc, h);
+    }
+    *reinterpret_cast<float4*>(a + v * Hp + n) = acc;
+  }
+}
+
+hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
+                                int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
+                                int64_t N, int H, int Hp, int act, float* h0, float* pre0,
+                                float* a, hipStream_t st) {
+  if (N <= 0) return hipSuccess;
+  if (Hp % 4 || Hp / 4 > 128) return hipErrorInvalidValue;  // one thread per float4 column
+  const int threads = (Hp / 4 + 63) / 64 * 64;
+  const int nb = (int)cdiv(N, kEiNodes);
+  if (Fe <= kEiMaxFe && (Fe == 0 || Fep % 4 == 0))
+    hipLaunchKernelGGL(k_edge_init_seg<true>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
+  else
+    hipLaunchKernelGGL(k_edge_init_seg<false>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------
 // add-pool + ffn head (GNN.py:110): one workgroup per graph
 // ------------------------------------------------------------------------------------------

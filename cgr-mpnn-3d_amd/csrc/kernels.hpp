@@ -26,6 +26,11 @@ struct TransposeJobs {
 hipError_t transpose_batch(const TransposeJobs& jobs, hipStream_t st);
 
 // h0 = act(P[src_s] + e_s @ W0e^T + b0) ; pre0 stored if non-null
+// edge init + a_0 = segsum_dst(h0) in one pass (Hp <= 512); hipErrorInvalidValue otherwise
+hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
+                                int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
+                                int64_t N, int H, int Hp, int act, float* h0, float* pre0,
+                                float* a, hipStream_t st);
 hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int Fe, int Fep,
                          const float* w0eT, const float* b0, int64_t E, int H, int Hp, int act,
                          float* h0, float* pre0, hipStream_t st);
