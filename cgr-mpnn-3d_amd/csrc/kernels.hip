@@ -179,7 +179,10 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
 // all those edges (the per-edge kernel reloaded it for every edge: 14 float4 + 14 scalar loads
 // per output float4), and sums its edges' h0 into a_0 in edge order -- the same adds, in the same
 // order, as k_edge_init followed by k_segsum_v4<false>, so h0 / pre0 / a_0 are bitwise unchanged.
-constexpr int kEiNodes = 4;
+#ifndef CGR_EI_NODES
+#define CGR_EI_NODES 4
+#endif
+constexpr int kEiNodes = CGR_EI_NODES;
 constexpr int kEiMaxFe = 16;
 
 template <bool REG>
