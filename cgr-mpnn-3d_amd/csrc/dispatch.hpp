@@ -39,6 +39,14 @@ inline auto with_nt_rn(int N, F&& f) {
   return f(IC<4>{});
 }
 
+// x-GEMM k-tile depth (BK = 16 * KT) and the waves of the node-row (N-row) NT GEMMs
+#ifndef CGR_XGEMM_KT
+#define CGR_XGEMM_KT 2
+#endif
+#ifndef CGR_NODE_NT_WAVES
+#define CGR_NODE_NT_WAVES 4
+#endif
+
 // Edge-row (layer) NT GEMMs: (WAVES, RN).  Default 4 waves x 5 fragments (64 x 80 tiles) when
 // H tiles by 80; CGR_NT_WIDE selects 8 waves x 13 fragments (128 x 208 tiles) for A/B runs.
 #ifndef CGR_NT_WIDE

@@ -118,7 +118,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dzn, Hp};
       LdPlain<4> bl{wT + D * HHp, Hp};
       EpStore ep{ds, Hp, N, H, nullptr};
-      return launch_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, N, H, H, st);
+      return launch_nt<CGR_NODE_NT_WAVES, 1, decltype(RN)::value, 1>(al, bl, ep, N, H, H, st);
     });
     HIP_RET(e);
   }

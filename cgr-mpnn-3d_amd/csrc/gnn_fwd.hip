@@ -117,7 +117,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
             LdPlain<decltype(VX)::value> al{xa, ldx};
             LdPlain<decltype(VW)::value> bl{Wb, ldw};
             EpStore ep{part == 0 ? fv.P : fv.Q, Hp, N, H, nullptr};
-            return launch_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, H, F, side);
+            return launch_nt<4, 1, decltype(RN)::value, CGR_XGEMM_KT>(al, bl, ep, N, H, F, side);
           });
         });
       });
@@ -134,7 +134,8 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
             LdPlain<decltype(VX)::value> al{xa, ldx};
             LdTwoRows<decltype(VB)::value> bl{W0, F + Fe, Wn, F + H, H};
             EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
-            return launch_nt<4, 1, decltype(RN)::value, 2>(al, bl, ep, N, 2 * H, F, side);
+            return launch_nt<4, 1, decltype(RN)::value, CGR_XGEMM_KT>(al, bl, ep, N, 2 * H, F,
+                                                                      side);
           });
         });
       });
@@ -237,7 +238,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       return with_nt_rn(H, [&](auto RN) {
         LdPlain<4> al{fv.a[D], Hp};
         LdPlain<decltype(VW)::value> blw{Wn + F, F + H};
-        return launch_nt<4, 1, decltype(RN)::value, 1>(al, blw, ep, N, H, H, st);
+        return launch_nt<CGR_NODE_NT_WAVES, 1, decltype(RN)::value, 1>(al, blw, ep, N, H, H, st);
       });
     });
     HIP_RET(e);
