@@ -463,3 +463,36 @@ def test_cuda_graph_capture_replays_fwd_bwd(cuda_device):
     assert torch.equal(gp, eager_pred)
     for a, c in zip(gg, eager_g):
         assert torch.equal(a, c)
+
+
+def _sparse_batch(num_graphs, n_atoms, seed):
+    """Reactions whose atoms are mostly unbonded: per graph a 3-bond chain 0-1-2-3 plus a bond
+    from atom 0 to the last atom (the reference needs the batch's last node to have an incoming
+    edge), so N = n_atoms * B far exceeds E = 8 * B.  Exercises the backward's fused segmented
+    sum + activation kernel with node segments that have no edges and the learnable-skip partial
+    sums sized by max(E, N)."""
+    from cgr_mpnn_3D._amd.synth import RxnBatch
+
+    rng = np.random.default_rng(seed)
+    xs, eis, eas, bt = [], [], [], []
+    for g in range(num_graphs):
+        off = g * n_atoms
+        pairs = [(0, 1), (1, 2), (2, 3), (0, n_atoms - 1)]
+        ei = []
+        for a, c in pairs:
+            ei += [(off + a, off + c), (off + c, off + a)]
+        eis.append(np.array(ei, np.int64).T)
+        xs.append(rng.standard_normal((n_atoms, 21)).astype(np.float32))
+        eas.append(rng.standard_normal((len(ei), 14)).astype(np.float32))
+        bt.append(np.full(n_atoms, g, np.int64))
+    ptr = np.arange(num_graphs + 1, dtype=np.int64) * n_atoms
+    y = rng.normal(80.0, 20.0, num_graphs).astype(np.float32)
+    return RxnBatch(x=np.concatenate(xs), edge_index=np.concatenate(eis, 1),
+                    edge_attr=np.concatenate(eas), batch=np.concatenate(bt), ptr=ptr, y=y)
+
+
+@pytest.mark.parametrize("act,skip", [("relu", True), ("silu", True), ("relu", False)])
+def test_mostly_unbonded_atoms_vs_oracle(act, skip, cuda_device):
+    b = _sparse_batch(6, 40, seed=27)
+    assert b.x.shape[0] > b.edge_index.shape[1]
+    _oracle_compare(b, 64, 3, act, skip, cuda_device)
