@@ -79,7 +79,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
-  hipStream_t side = prof_enabled() ? st : ss->side;
+  hipStream_t side = (prof_enabled() || single_stream()) ? st : ss->side;
 
   // head + readout
   {

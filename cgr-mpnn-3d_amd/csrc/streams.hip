@@ -1,5 +1,7 @@
 #include "streams.hpp"
 
+#include <stdlib.h>
+
 #include <mutex>
 #include <string>
 
@@ -11,6 +13,14 @@ namespace {
 std::mutex g_mu;
 SideStreams* g_side[64] = {nullptr};
 }  // namespace
+
+bool single_stream() {
+  static const bool on = [] {
+    const char* v = getenv("CGR_SINGLE_STREAM");
+    return v && v[0] == '1';
+  }();
+  return on;
+}
 
 SideStreams* side_streams(hipStream_t main) {
   int dev = 0;

@@ -15,6 +15,10 @@ struct SideStreams {
   int next;
 };
 
+// CGR_SINGLE_STREAM=1 in the environment: everything on the caller's stream (A/B of the
+// side-stream concurrency against the cross-queue dependency latency it adds in a graph)
+bool single_stream();
+
 // returns nullptr and sets the library error if the streams cannot be created
 SideStreams* side_streams(hipStream_t main);
 
