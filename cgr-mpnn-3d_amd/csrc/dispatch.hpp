@@ -8,6 +8,7 @@
 #include "gemm.hpp"
 #include "gemm_tn.hpp"
 #include "gemm_x3.hpp"
+#include "gemm_rs.hpp"
 
 namespace cgr {
 
@@ -100,6 +101,40 @@ inline hipError_t launch_nt(const AL& al, const BL& bl, const EP& ep, int M, int
 #else
   return launch_gemm_nt<W, RM, RN, KT>(al, bl, ep, M, N, K, st);
 #endif
+}
+
+// Edge-row layer GEMMs (E x H x H) on the row-block-stationary kernel (gemm_rs.hpp) when the
+// shape allows it: lab A/B at cfg2 59 us vs 66-68 us for the 64x80-tile kernel, bitwise-equal
+// output (same k order per output).  CGR_RS_LAYER=0 builds the tiled kernel only.
+#ifndef CGR_RS_LAYER
+#define CGR_RS_LAYER 1
+#endif
+#ifndef CGR_RS_BWD
+#define CGR_RS_BWD 0  // 1: also the layer backward NT (dm = dpre W_l); A/B: no gain beside the side-stream TN kernels (one 1024-thread WG per CU co-schedules poorly)
+#endif
+#ifndef CGR_RS_RM
+#define CGR_RS_RM 2
+#endif
+inline bool use_rs(int N, int K, int64_t ldb, const void* B) {
+  if (!CGR_RS_LAYER || CGR_GEMM_X3 || !rs_ok(N, K, ldb, B)) return false;
+  const int f = rs_fmax(N, CGR_RS_RM);
+  return CGR_RS_RM == 2 ? (f == 1 || f == 4) : (f == 2 || f == 7 || f == 8);
+}
+template <class F>
+inline hipError_t with_rs_fmax(int N, F&& f) {
+#if CGR_RS_RM == 2
+  switch (rs_fmax(N, 2)) {
+    case 1: return f(IC<1>{});
+    case 4: return f(IC<4>{});
+  }
+#else
+  switch (rs_fmax(N, 1)) {
+    case 2: return f(IC<2>{});
+    case 7: return f(IC<7>{});
+    case 8: return f(IC<8>{});
+  }
+#endif
+  return hipErrorInvalidValue;
 }
 
 inline TnPlan tn_plan(int Nout, int Kout, int R) {

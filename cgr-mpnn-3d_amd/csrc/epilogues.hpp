@@ -33,10 +33,34 @@ struct EpStore {
       if (c + 3 < N) o[3] = v.w;
     }
   }
-  struct Pre {};
-  __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
-  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&) const {
-    apply4(r, c, v);
+  // prefetched epilogue operands (gemm_nt_kernel issues every pre4 load of a tile before the
+  // accumulators go through LDS, so the loads overlap instead of one round trip per float4)
+  struct Ctx {};
+  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  typedef float4 Pre;
+  __device__ __forceinline__ Pre pre4(int r, int c) const {
+    if (!bias) return f4zero();
+    return make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
+                       bias[min(c + 3, N - 1)]);
+  }
+  // scalar form (row-stationary kernel: one accumulator element per call)
+  typedef float Pre1;
+  __device__ __forceinline__ Pre1 pre1(int r, int c) const { return bias ? bias[min(c, N - 1)] : 0.f; }
+  __device__ __forceinline__ void apply1p(int r, int c, float v, Pre1 b, const Ctx&) const {
+    if (r < M && c < N) C[(int64_t)r * ld + c] = v + b;
+  }
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& b, const Ctx&) const {
+    if (r >= M || c >= N) return;
+    v = f4add(v, b);
+    float* o = C + (int64_t)r * ld + c;
+    if (c + 4 <= N && ((ld & 3) == 0)) {
+      *reinterpret_cast<float4*>(o) = v;
+    } else {
+      o[0] = v.x;
+      if (c + 1 < N) o[1] = v.y;
+      if (c + 2 < N) o[2] = v.z;
+      if (c + 3 < N) o[3] = v.w;
+    }
   }
 };
 
@@ -70,32 +94,63 @@ struct EpLayer {
   // internal [M, ld] buffers, ld % 4 == 0: whole float4 in bounds of the padded row; columns >= N
   // hold don't-care values (never read as data)
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
-    if (r >= M || c >= N) return;
-    apply4p(r, c, v, *reinterpret_cast<const float4*>(h0 + (int64_t)r * ld + c));
+    apply4p(r, c, v, pre4(r, c), ctx());
   }
-  // h0 prefetch: unconditional load from a clamped in-bounds address (no branch around the load)
-  typedef float4 Pre;
+  // prefetch: h0 and bias of a float4 piece, unconditional loads from clamped in-bounds addresses
+  // (no branch around the loads); the scalars (sigma, dropout key) once per workgroup
+  struct Ctx {
+    float sg;
+    uint64_t key;
+  };
+  __device__ __forceinline__ Ctx ctx() const {
+    return Ctx{sigma ? sigma[0] : 1.f, thresh ? *seed : 0ull};
+  }
+  struct Pre {
+    float4 h0, b;
+  };
   __device__ __forceinline__ Pre pre4(int r, int c) const {
     const bool ok = r < M && c < N;
-    return *reinterpret_cast<const float4*>(h0 + (ok ? (int64_t)r * ld + c : 0));
+    return Pre{*reinterpret_cast<const float4*>(h0 + (ok ? (int64_t)r * ld + c : 0)),
+               make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
+                           bias[min(c + 3, N - 1)])};
   }
-  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& hz) const {
+  struct Pre1 {
+    float h0, b;
+  };
+  __device__ __forceinline__ Pre1 pre1(int r, int c) const {
+    const bool ok = r < M && c < N;
+    return Pre1{h0[ok ? (int64_t)r * ld + c : 0], bias[min(c, N - 1)]};
+  }
+  __device__ __forceinline__ void apply1p(int r, int c, float v, const Pre1& p,
+                                          const Ctx& cx) const {
     if (r >= M || c >= N) return;
     const int64_t o = (int64_t)r * ld + c;
-    const float sg = sigma ? sigma[0] : 1.f;
+    const float z = (v + p.b) + cx.sg * p.h0;
+    if (pre) pre[o] = z;
+    float h = act_fwd(z, act);
+    if (thresh)
+      h = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c, thresh) ? h * scale : 0.f;
+    else
+      h *= scale;
+    hout[o] = h;
+  }
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& p,
+                                          const Ctx& cx) const {
+    if (r >= M || c >= N) return;
+    const int64_t o = (int64_t)r * ld + c;
     float z[4] = {v.x, v.y, v.z, v.w};
-    const float h0v[4] = {hz.x, hz.y, hz.z, hz.w};
+    const float h0v[4] = {p.h0.x, p.h0.y, p.h0.z, p.h0.w};
+    const float bv[4] = {p.b.x, p.b.y, p.b.z, p.b.w};
 #pragma unroll
-    for (int k = 0; k < 4; ++k) z[k] = (z[k] + bias[min(c + k, N - 1)]) + sg * h0v[k];
+    for (int k = 0; k < 4; ++k) z[k] = (z[k] + bv[k]) + cx.sg * h0v[k];
     if (pre) *reinterpret_cast<float4*>(pre + o) = make_float4(z[0], z[1], z[2], z[3]);
     float h[4];
-    const uint64_t key = thresh ? *seed : 0;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       h[k] = act_fwd(z[k], act);
       if (thresh)
-        h[k] = drop_keep(key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
-                                                                                 : 0.f;
+        h[k] = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
+                                                                                    : 0.f;
       else
         h[k] *= scale;
     }
@@ -126,9 +181,11 @@ struct EpSplit2 {
       }
     }
   }
+  struct Ctx {};
+  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
   struct Pre {};
   __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
-  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&) const {
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&, const Ctx&) const {
     apply4(r, c, v);
   }
 };
@@ -142,24 +199,29 @@ struct EpReadoutQ {
   int64_t ld;
   int M, N;
   int act;
-  typedef float4 Pre;
+  struct Ctx {};
+  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  struct Pre {
+    float4 q, b;
+  };
   __device__ __forceinline__ Pre pre4(int r, int c) const {
     const bool ok = r < M && c < N;
-    return *reinterpret_cast<const float4*>(Q + (ok ? (int64_t)r * ld + c : 0));
+    return Pre{*reinterpret_cast<const float4*>(Q + (ok ? (int64_t)r * ld + c : 0)),
+               make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
+                           bias[min(c + 3, N - 1)])};
   }
-  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& q) const {
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& p,
+                                          const Ctx&) const {
     if (r >= M || c >= N) return;
     const int64_t o = (int64_t)r * ld + c;
-    float z[4] = {v.x + q.x, v.y + q.y, v.z + q.z, v.w + q.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) z[k] += bias[min(c + k, N - 1)];
+    const float4 z4 = f4add(f4add(v, p.q), p.b);
+    const float z[4] = {z4.x, z4.y, z4.z, z4.w};
     if (zn) *reinterpret_cast<float4*>(zn + o) = make_float4(z[0], z[1], z[2], z[3]);
     *reinterpret_cast<float4*>(hn + o) =
         make_float4(act_fwd(z[0], act), act_fwd(z[1], act), act_fwd(z[2], act), act_fwd(z[3], act));
   }
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
-    if (r >= M || c >= N) return;
-    apply4p(r, c, v, *reinterpret_cast<const float4*>(Q + (int64_t)r * ld + c));
+    apply4p(r, c, v, pre4(r, c), ctx());
   }
 };
 
@@ -188,9 +250,11 @@ struct EpReadout {
     *reinterpret_cast<float4*>(hn + o) =
         make_float4(act_fwd(z[0], act), act_fwd(z[1], act), act_fwd(z[2], act), act_fwd(z[3], act));
   }
+  struct Ctx {};
+  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
   struct Pre {};
   __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
-  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&) const {
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&, const Ctx&) const {
     apply4(r, c, v);
   }
 };

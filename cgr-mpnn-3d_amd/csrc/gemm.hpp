@@ -251,9 +251,11 @@ struct NTShape {
   static_assert(ACH % NT == 0, "A chunks per thread must be integral");
 };
 
-template <int WAVES, int RM, int RN, int KT, int PF, class AL, class BL, class EP>
-__global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N,
-                                                             int K, int tiles_n) {
+// OCC > 0 asks the compiler for OCC waves per SIMD (register budget 512 / OCC per lane)
+template <int WAVES, int RM, int RN, int KT, int PF, int OCC, class AL, class BL, class EP>
+__global__ __attribute__((amdgpu_flat_work_group_size(1, WAVES * 64),
+                          amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void
+gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int K, int tiles_n) {
   using S = NTShape<WAVES, RM, RN, KT>;
   constexpr int NT = S::NT, BM = S::BM, BN = S::BN, BK = S::BK, CPR = S::CPR;
   constexpr int ACH = S::ACH, BCH = S::BCH, APT = S::APT, BPT = S::BPT;
@@ -385,7 +387,20 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep
     }
   }
 
-  // epilogue: accumulators -> LDS [BM][LDC] -> coalesced float4 rows -> ep.apply4
+  // epilogue: accumulators -> LDS [BM][LDC] -> coalesced float4 rows -> ep.apply4p.  Every
+  // operand load of the epilogue (h0 / Q rows, bias) is issued first, from clamped in-bounds
+  // addresses, so they land while the accumulators go through LDS: one memory round trip per
+  // tile instead of one per float4 piece.
+  constexpr int C4 = BN / 4;
+  constexpr int EIT = (BM * C4 + NT - 1) / NT;
+  const typename EP::Ctx cx = ep.ctx();
+  typename EP::Pre pv[EIT];
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int q = min(tid + it * NT, BM * C4 - 1);
+    const int r = q / C4, c4 = q - r * C4;
+    pv[it] = ep.pre4(m0 + r, n0 + 4 * c4);
+  }
   float* C = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int i = 0; i < RM; ++i)
@@ -395,21 +410,24 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_nt_kernel(AL al, BL bl, EP ep
       for (int r = 0; r < 4; ++r)
         C[(w * 16 * RM + i * 16 + fg * 4 + r) * S::LDC + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
-  constexpr int C4 = BN / 4;
-  for (int q = tid; q < BM * C4; q += NT) {
-    const int r = q / C4, c4 = q - r * C4;
-    const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
-    ep.apply4(m0 + r, n0 + 4 * c4, v);
+#pragma unroll
+  for (int it = 0; it < EIT; ++it) {
+    const int q = tid + it * NT;
+    if (q < BM * C4) {
+      const int r = q / C4, c4 = q - r * C4;
+      const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
+      ep.apply4p(m0 + r, n0 + 4 * c4, v, pv[it], cx);
+    }
   }
 }
 
-template <int WAVES, int RM, int RN, int KT, class AL, class BL, class EP, int PF = 2>
+template <int WAVES, int RM, int RN, int KT, class AL, class BL, class EP, int PF = 2, int OCC = 0>
 inline hipError_t launch_gemm_nt(const AL& al, const BL& bl, const EP& ep, int M, int N, int K,
                                  hipStream_t st) {
   using S = NTShape<WAVES, RM, RN, KT>;
   if (M <= 0 || N <= 0) return hipSuccess;
   const int tm = (M + S::BM - 1) / S::BM, tn = (N + S::BN - 1) / S::BN;
-  hipLaunchKernelGGL((gemm_nt_kernel<WAVES, RM, RN, KT, PF, AL, BL, EP>), dim3(tm * tn),
+  hipLaunchKernelGGL((gemm_nt_kernel<WAVES, RM, RN, KT, PF, OCC, AL, BL, EP>), dim3(tm * tn),
                      dim3(WAVES * 64), 0, st, al, bl, ep, M, N, K, tn);
   return hipGetLastError();
 }

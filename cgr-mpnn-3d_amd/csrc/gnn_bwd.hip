@@ -175,7 +175,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     // main: dm = dpre W_l
     {
       ProfScope _p("gemm_nt_layer_bwd", st);
-      hipError_t e = with_nt_layer(H, [&](auto WV, auto RN) {
+      hipError_t e = CGR_RS_BWD && use_rs(H, H, Hp, wT + l * HHp) ? with_rs_fmax(H, [&](auto FM) {
+        LdPlain<4> al{dp, Hp};
+        EpStore ep{dm, Hp, E, H, nullptr};
+        return launch_gemm_rs<CGR_RS_RM, decltype(FM)::value>(al, wT + l * HHp, Hp, ep, E, H, H, st);
+      }) : with_nt_layer(H, [&](auto WV, auto RN) {
         LdPlain<4> al{dp, Hp};
         LdPlain<4> bl{wT + l * HHp, Hp};
         EpStore ep{dm, Hp, E, H, nullptr};

@@ -213,7 +213,9 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     {
       ProfScope _p("gemm_nt_layer_fwd", st);
       const int vw = vec_for(Wl, H, H);
-      hipError_t e = with_vec(vw, [&](auto VW) {
+      hipError_t e = use_rs(H, H, H, Wl) ? with_rs_fmax(H, [&](auto FM) {
+        return launch_gemm_rs<CGR_RS_RM, decltype(FM)::value>(al, Wl, H, ep, E, H, H, st);
+      }) : with_vec(vw, [&](auto VW) {
         return with_nt_layer(H, [&](auto WV, auto RN) {
           LdPlain<decltype(VW)::value> blw{Wl, H};
           return launch_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, blw, ep, E,
