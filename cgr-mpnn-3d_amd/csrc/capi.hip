@@ -166,11 +166,18 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     slab = s > slab ? s : slab;
     bslab = bs > bslab ? bs : bslab;
   };
-  // side-stream TN GEMMs (readout, layers, edge features) share one slab; the main-stream TN
-  // (x-part of edge init) runs concurrently with the last of them and gets its own
-  acc(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N);  // readout TN runs over [xp | s] when padded
-  acc(d.H, d.H, d.E);
-  if (d.Fe > 0) acc(d.H, d.Fe, d.E);
+  // side-stream TN GEMMs (readout, layers, edge features): with batched reduction each gets its
+  // own slab (reduced together in one launch at the end of the side stream), otherwise they share
+  // one; the main-stream TN (x-part of edge init) runs beside them and always gets its own
+  auto side = [&](int Nout, int Kout, int64_t R) {
+    if (!CGR_BATCH_REDUCE) return acc(Nout, Kout, R);
+    const TnPlan p = tn_plan(Nout, Kout, (int)R);
+    slab += (size_t)p.splits * Nout * (size_t)((Kout + 3) & ~3);
+    bslab += (size_t)p.splits * Nout;
+  };
+  side(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N);  // readout TN runs over [xp | s] when padded
+  for (int l = 0; l < (CGR_BATCH_REDUCE ? d.D : 1); ++l) side(d.H, d.H, d.E);
+  if (d.Fe > 0) side(d.H, d.Fe, d.E);
   W.slab_elems = slab;
   W.bslab_elems = bslab;
   W.slab = b.take(4 * slab);

@@ -117,6 +117,8 @@ inline hipError_t launch_nt(const AL& al, const BL& bl, const EP& ep, int M, int
 #endif
 inline bool use_rs(int N, int K, int64_t ldb, const void* B) {
   if (!CGR_RS_LAYER || CGR_GEMM_X3 || !rs_ok(N, K, ldb, B)) return false;
+  // every column group needs >= 1 fragment: all 16 waves produce A chunks and meet the barriers
+  if ((N + 15) / 16 < 4 * CGR_RS_RM) return false;
   const int f = rs_fmax(N, CGR_RS_RM);
   return CGR_RS_RM == 2 ? (f == 1 || f == 4) : (f == 2 || f == 7 || f == 8);
 }

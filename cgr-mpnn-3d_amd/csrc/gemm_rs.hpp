@@ -260,6 +260,8 @@ inline size_t rs_lds_bytes(int N, int K) {
 
 // B: [N, ldb] row-major weight rows (n, k), 16-byte aligned rows (ldb % 4 == 0), K % 4 == 0,
 // N % 16 == 0, N <= 64 * FMAX, K <= RS_KMAX, N * ldb < 2^31 (rs_ok checks these).
+// (the dispatcher also requires ceil(N / 16) >= 4 * RM: a wave group without a column fragment
+// would skip the A-chunk production and the barriers)
 inline bool rs_ok(int N, int K, int64_t ldb, const void* B) {
   return N > 0 && N % 16 == 0 && N <= RS_NMAX && K % 4 == 0 && K <= RS_KMAX && ldb % 4 == 0 &&
          ((uintptr_t)B & 15) == 0 && (int64_t)N * ldb < (int64_t(1) << 31);

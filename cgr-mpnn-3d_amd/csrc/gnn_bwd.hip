@@ -43,9 +43,16 @@ static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout
   });
 }
 
+// jobs != nullptr: queue the reduction for one batched launch (CGR_BATCH_REDUCE) instead
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
                             int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
-                            hipStream_t st, int gap_at = 0, int gap_len = 0) {
+                            hipStream_t st, int gap_at = 0, int gap_len = 0,
+                            RedJobs* jobs = nullptr) {
+  if (jobs)
+    return add_reduce_job(*jobs, slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off,
+                          bias_dst, gap_at, gap_len)
+               ? hipSuccess
+               : hipErrorInvalidValue;
   ProfScope _p("splitk_reduce", st);
   return reduce_slabs(slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, st,
                       gap_at, gap_len);
@@ -78,6 +85,21 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
 
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
+  // side-stream slabs: consecutive regions when batched (workspace_layout sizes them in the same
+  // order: readout, layers D-1 .. 0, edge), else all at the start of the shared region
+  RedJobs side_jobs{};
+  float* slab_next = slab;
+  float* bslab_next = bslab;
+  auto side_slab = [&](int Nout, int Kout, int64_t R, float** sp, float** bp) {
+    *sp = slab_next;
+    *bp = bslab_next;
+    if (CGR_BATCH_REDUCE) {
+      const TnPlan q = tn_plan(Nout, Kout, (int)R);
+      slab_next += (size_t)q.splits * Nout * (size_t)((Kout + 3) & ~3);
+      bslab_next += (size_t)q.splits * Nout;
+    }
+  };
+  RedJobs* sj = CGR_BATCH_REDUCE ? &side_jobs : nullptr;
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
   hipStream_t side = (prof_enabled() || single_stream()) ? st : ss->side;
 
@@ -94,22 +116,26 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   if (fv.xp) {  // [xp | s] with x padded to Fp: the pad columns are skipped by the reduce
     const int Fp = d.Fp;
     TnPlan p;
+    float *rsl, *rbs;
+    side_slab(H, Fp + H, N, &rsl, &rbs);
     LdPlain<4> al{dzn, Hp};
     LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
-    HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, slab, bslab, true, &p, side));
-    HIP_RET(tn_reduce(p, slab, bslab, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
-                      grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F));
+    HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side));
+    HIP_RET(tn_reduce(p, rsl, rbs, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
+                      grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F, sj));
   } else {
     const int vx = vec_for(b->x, F, F);
     TnPlan p;
+    float *rsl, *rbs;
+    side_slab(H, F + H, N, &rsl, &rbs);
     hipError_t e = with_vec(vx, [&](auto VX) {
       LdPlain<4> al{dzn, Hp};
       LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
-      return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, slab, bslab, true, &p, side);
+      return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, rsl, rbs, true, &p, side);
     });
     HIP_RET(e);
-    HIP_RET(tn_reduce(p, slab, bslab, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
-                      grads[CGR_PARAM_E2N_B(D)], side));
+    HIP_RET(tn_reduce(p, rsl, rbs, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
+                      grads[CGR_PARAM_E2N_B(D)], side, 0, 0, sj));
   }
   // main: ds = dzn W_n[:, F:]
   {
@@ -167,10 +193,12 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dp, Hp};
       LdGatherDiff<false> bl{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
       TnPlan p;
-      HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, slab, bslab, true, &p, side));
+      float *lsl, *lbs;
+      side_slab(H, H, E, &lsl, &lbs);
+      HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, lsl, lbs, true, &p, side));
       HIP_RET(record_point(ss, side, &tn_done[l]));
-      HIP_RET(tn_reduce(p, slab, bslab, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
-                        grads[CGR_PARAM_CONV_B(l)], side));
+      HIP_RET(tn_reduce(p, lsl, lbs, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
+                        grads[CGR_PARAM_CONV_B(l)], side, 0, 0, sj));
     }
     // main: dm = dpre W_l
     {
@@ -218,8 +246,14 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     LdPlain<4> al{dpre0, Hp};
     LdPlain<4> bl{fv.e_s, d.Fep};
     TnPlan p;
-    HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, slab, bslab, true, &p, side));
-    HIP_RET(tn_reduce(p, slab, bslab, H, Fe, gW0, F + Fe, F, gb0, side));
+    float *esl, *ebs;
+    side_slab(H, Fe, E, &esl, &ebs);
+    HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, esl, ebs, true, &p, side));
+    HIP_RET(tn_reduce(p, esl, ebs, H, Fe, gW0, F + Fe, F, gb0, side, 0, 0, sj));
+  }
+  if (sj) {  // every side-stream weight gradient, one launch, at the end of the side stream
+    ProfScope _p("splitk_reduce", side);
+    HIP_RET(reduce_slabs_batched(side_jobs, CGR_BATCH_REDUCE_BLOCKS, side));
   }
   {
     ProfScope _p("segsum_src_bwd", st);

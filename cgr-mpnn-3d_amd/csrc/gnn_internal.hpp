@@ -99,6 +99,15 @@ struct ArenaLayout {
       g;
 };
 
+// 1: every side-stream weight gradient gets its own split-K slab and all of them are reduced in
+// one batched launch at the end of the side stream; 0: one shared slab, reduced after each GEMM.
+// Same-box A/B: batched 1.44 ms/step vs 1.34 ms (256 / 4096 blocks no better), so 0.
+#ifndef CGR_BATCH_REDUCE
+#define CGR_BATCH_REDUCE 0
+#endif
+#ifndef CGR_BATCH_REDUCE_BLOCKS
+#define CGR_BATCH_REDUCE_BLOCKS 1024
+#endif
 struct WorkspaceLayout {
   size_t bytes;
   size_t dpre[2], dm, dh0, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,

@@ -632,88 +632,118 @@ constexpr int kRedCols = 32, kRedGroups = 8;
 #define CGR_REDUCE_MAX_BLOCKS 256  // A/B: 256 beats 64 and unbounded (4096) by 4-8 %
 #endif
 
-__global__ __launch_bounds__(kRedCols * kRedGroups) void k_reduce_slabs(
-    const float* __restrict__ slab, const float* __restrict__ bslab, int splits, int Nout,
-    int Kout, float* __restrict__ dst, int64_t ld_dst, int64_t col_off, float* __restrict__ bias_dst,
-    int main_blocks, int gap_at, int gap_len) {
-  __shared__ float4 part[kRedGroups][kRedCols];
-  __shared__ float bpart[kRedGroups][kRedCols];
+// one logical block of one reduction job
+__device__ __forceinline__ void reduce_slab_block(const RedJob& J, int blk, float4 (*part)[kRedCols],
+                                                  float (*bpart)[kRedCols]) {
   const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
-  const int ldk = (Kout + 3) & ~3;
+  const int ldk = (J.Kout + 3) & ~3;
   const int c4n = ldk >> 2;
-  const int64_t nf = (int64_t)Nout * c4n;
-  const int nblk = main_blocks + (bias_dst ? (Nout + kRedCols - 1) / kRedCols : 0);
-  // grid-stride over the logical blocks: the launch is kept narrow (it runs on the side stream
-  // beside the critical path; a wide launch would take every CU's slots from it)
-  for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-    if (blk < main_blocks) {
-      const int64_t f = (int64_t)blk * kRedCols + col;
-      float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (f < nf) {
-        const float4* s4 = reinterpret_cast<const float4*>(slab) + f;
+  const int64_t nf = (int64_t)J.Nout * c4n;
+  if (blk < J.main_blocks) {
+    const int64_t f = (int64_t)blk * kRedCols + col;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (f < nf) {
+      const float4* s4 = reinterpret_cast<const float4*>(J.slab) + f;
 #pragma unroll 4
-        for (int p = grp; p < splits; p += kRedGroups) {
-          const float4 v = s4[(int64_t)p * nf];
-          s.x += v.x;
-          s.y += v.y;
-          s.z += v.z;
-          s.w += v.w;
-        }
-      }
-      part[grp][col] = s;
-      __syncthreads();
-      if (grp == 0 && f < nf) {
-        float4 t = part[0][col];
-#pragma unroll
-        for (int g = 1; g < kRedGroups; ++g) {
-          const float4 u = part[g][col];
-          t.x += u.x;
-          t.y += u.y;
-          t.z += u.z;
-          t.w += u.w;
-        }
-        const int64_t n = f / c4n;
-        const int k = (int)(f - n * c4n) * 4;
-        float* o = dst + n * ld_dst + col_off;
-        const float tv[4] = {t.x, t.y, t.z, t.w};
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int kk = k + q;
-          if (kk >= Kout || (kk >= gap_at && kk < gap_at + gap_len)) continue;
-          o[kk >= gap_at + gap_len ? kk - gap_len : kk] = tv[q];
-        }
-      }
-    } else {
-      const int64_t n = (int64_t)(blk - main_blocks) * kRedCols + col;
-      float s = 0.f;
-      if (n < Nout)
-        for (int p = grp; p < splits; p += kRedGroups) s += bslab[(int64_t)p * Nout + n];
-      bpart[grp][col] = s;
-      __syncthreads();
-      if (grp == 0 && n < Nout) {
-        float t = bpart[0][col];
-#pragma unroll
-        for (int g = 1; g < kRedGroups; ++g) t += bpart[g][col];
-        bias_dst[n] = t;
+      for (int p = grp; p < J.splits; p += kRedGroups) {
+        const float4 v = s4[(int64_t)p * nf];
+        s.x += v.x;
+        s.y += v.y;
+        s.z += v.z;
+        s.w += v.w;
       }
     }
-    __syncthreads();  // part / bpart reused by the next logical block
+    part[grp][col] = s;
+    __syncthreads();
+    if (grp == 0 && f < nf) {
+      float4 t = part[0][col];
+#pragma unroll
+      for (int g = 1; g < kRedGroups; ++g) {
+        const float4 u = part[g][col];
+        t.x += u.x;
+        t.y += u.y;
+        t.z += u.z;
+        t.w += u.w;
+      }
+      const int64_t n = f / c4n;
+      const int k = (int)(f - n * c4n) * 4;
+      float* o = J.dst + n * J.ld_dst + J.col_off;
+      const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int kk = k + q;
+        if (kk >= J.Kout || (kk >= J.gap_at && kk < J.gap_at + J.gap_len)) continue;
+        o[kk >= J.gap_at + J.gap_len ? kk - J.gap_len : kk] = tv[q];
+      }
+    }
+  } else {
+    const int n = (blk - J.main_blocks) * kRedCols + col;
+    float s = 0.f;
+    if (n < J.Nout)
+      for (int p = grp; p < J.splits; p += kRedGroups) s += J.bslab[(int64_t)p * J.Nout + n];
+    bpart[grp][col] = s;
+    __syncthreads();
+    if (grp == 0 && n < J.Nout) {
+      float t = bpart[0][col];
+#pragma unroll
+      for (int g = 1; g < kRedGroups; ++g) t += bpart[g][col];
+      J.bias_dst[n] = t;
+    }
   }
+  __syncthreads();  // part / bpart reused by the next logical block
+}
+
+// several reductions in one launch (the backward batches every side-stream weight gradient):
+// logical blocks are numbered job by job; the grid strides over all of them
+__global__ __launch_bounds__(kRedCols * kRedGroups) void k_reduce_slabs(RedJobs jobs) {
+  __shared__ float4 part[kRedGroups][kRedCols];
+  __shared__ float bpart[kRedGroups][kRedCols];
+  for (int blk = blockIdx.x; blk < jobs.total; blk += gridDim.x) {
+    int j = 0, base = 0;
+    while (j + 1 < jobs.n && blk >= base + jobs.j[j].nblk) base += jobs.j[j++].nblk;
+    reduce_slab_block(jobs.j[j], blk - base, part, bpart);
+  }
+}
+
+bool add_reduce_job(RedJobs& jobs, const float* slab, const float* bslab, int splits, int Nout,
+                    int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
+                    int gap_at, int gap_len) {
+  const int64_t nf = (int64_t)Nout * (((Kout + 3) & ~3) >> 2);
+  if (nf <= 0) return true;
+  if (jobs.n >= kMaxRedJobs) return false;
+  RedJob& J = jobs.j[jobs.n++];
+  if (gap_len <= 0) gap_at = 0x7fffffff, gap_len = 0;
+  J.slab = slab;
+  J.bslab = bslab;
+  J.dst = dst;
+  J.bias_dst = bias_dst;
+  J.ld_dst = ld_dst;
+  J.col_off = col_off;
+  J.splits = splits;
+  J.Nout = Nout;
+  J.Kout = Kout;
+  J.gap_at = gap_at;
+  J.gap_len = gap_len;
+  J.main_blocks = (int)cdiv(nf, kRedCols);
+  J.nblk = J.main_blocks + (bias_dst ? (int)cdiv(Nout, kRedCols) : 0);
+  jobs.total += J.nblk;
+  return true;
+}
+
+hipError_t reduce_slabs_batched(const RedJobs& jobs, int max_blocks, hipStream_t st) {
+  if (jobs.n <= 0 || jobs.total <= 0) return hipSuccess;
+  const int grid = std::min(jobs.total, max_blocks);
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(grid), dim3(kRedCols * kRedGroups), 0, st, jobs);
+  return hipGetLastError();
 }
 
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                         hipStream_t st, int gap_at, int gap_len) {
-  const int64_t nf = (int64_t)Nout * (((Kout + 3) & ~3) >> 2);
-  if (gap_len <= 0) gap_at = 0x7fffffff, gap_len = 0;
-  if (nf <= 0) return hipSuccess;
-  const int main_blocks = (int)cdiv(nf, kRedCols);
-  const int bias_blocks = bias_dst ? (int)cdiv(Nout, kRedCols) : 0;
-  const int grid = std::min(main_blocks + bias_blocks, CGR_REDUCE_MAX_BLOCKS);
-  hipLaunchKernelGGL(k_reduce_slabs, dim3(grid), dim3(kRedCols * kRedGroups),
-                     0, st, slab, bslab, splits, Nout, Kout, dst, ld_dst, col_off, bias_dst,
-                     main_blocks, gap_at, gap_len);
-  return hipGetLastError();
+  RedJobs jobs{};
+  add_reduce_job(jobs, slab, bslab, splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, gap_at,
+                 gap_len);
+  return reduce_slabs_batched(jobs, CGR_REDUCE_MAX_BLOCKS, st);
 }
 
 __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int nb,

@@ -86,6 +86,24 @@ int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp);
 // dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
 // gap_len > 0: slab columns [gap_at, gap_at + gap_len) are padding and skipped; later columns
 // shift down by gap_len in dst (the x | s concat of the readout with x padded to 4 floats)
+// batched split-K slab reductions (one launch for several weight gradients)
+constexpr int kMaxRedJobs = 40;
+struct RedJob {
+  const float* slab;
+  const float* bslab;
+  float* dst;
+  float* bias_dst;
+  int64_t ld_dst, col_off;
+  int splits, Nout, Kout, gap_at, gap_len, main_blocks, nblk;
+};
+struct RedJobs {
+  RedJob j[kMaxRedJobs];
+  int n, total;
+};
+bool add_reduce_job(RedJobs& jobs, const float* slab, const float* bslab, int splits, int Nout,
+                    int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
+                    int gap_at = 0, int gap_len = 0);
+hipError_t reduce_slabs_batched(const RedJobs& jobs, int max_blocks, hipStream_t st);
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                         hipStream_t st, int gap_at = 0, int gap_len = 0);
