@@ -44,6 +44,10 @@ static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout
 }
 
 // jobs != nullptr: queue the reduction for one batched launch (CGR_BATCH_REDUCE) instead
+#ifndef CGR_RO_TN_AT
+#define CGR_RO_TN_AT -1
+#endif
+
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
                             int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                             hipStream_t st, int gap_at = 0, int gap_len = 0,
@@ -111,31 +115,41 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H, Hp,
                             d.act, dzn, st));
   }
-  // side: dW_n = dzn^T [x | s], db_n
-  HIP_RET(fork_to(ss, st, side));
-  if (fv.xp) {  // [xp | s] with x padded to Fp: the pad columns are skipped by the reduce
-    const int Fp = d.Fp;
-    TnPlan p;
-    float *rsl, *rbs;
-    side_slab(H, Fp + H, N, &rsl, &rbs);
-    LdPlain<4> al{dzn, Hp};
-    LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
-    HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side));
-    HIP_RET(tn_reduce(p, rsl, rbs, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
-                      grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F, sj));
-  } else {
-    const int vx = vec_for(b->x, F, F);
-    TnPlan p;
-    float *rsl, *rbs;
-    side_slab(H, F + H, N, &rsl, &rbs);
-    hipError_t e = with_vec(vx, [&](auto VX) {
+  // side: dW_n = dzn^T [x | s], db_n.  Enqueued here (CGR_RO_TN_AT < 0) or after the layer
+  // weight gradient of layer CGR_RO_TN_AT, so that it does not run beside the main stream's
+  // readout/top-layer GEMMs, which sit on the critical path
+  auto readout_tn = [&]() -> int {
+    HIP_RET(fork_to(ss, st, side));
+    if (fv.xp) {  // [xp | s] with x padded to Fp: the pad columns are skipped by the reduce
+      const int Fp = d.Fp;
+      TnPlan p;
+      float *rsl, *rbs;
+      side_slab(H, Fp + H, N, &rsl, &rbs);
       LdPlain<4> al{dzn, Hp};
-      LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
-      return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, rsl, rbs, true, &p, side);
-    });
-    HIP_RET(e);
-    HIP_RET(tn_reduce(p, rsl, rbs, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
-                      grads[CGR_PARAM_E2N_B(D)], side, 0, 0, sj));
+      LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
+      HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side));
+      HIP_RET(tn_reduce(p, rsl, rbs, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
+                        grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F, sj));
+    } else {
+      const int vx = vec_for(b->x, F, F);
+      TnPlan p;
+      float *rsl, *rbs;
+      side_slab(H, F + H, N, &rsl, &rbs);
+      hipError_t e = with_vec(vx, [&](auto VX) {
+        LdPlain<4> al{dzn, Hp};
+        LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
+        return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, rsl, rbs, true, &p, side);
+      });
+      HIP_RET(e);
+      HIP_RET(tn_reduce(p, rsl, rbs, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
+                        grads[CGR_PARAM_E2N_B(D)], side, 0, 0, sj));
+    }
+    return 0;
+  };
+  const int ro_at = (CGR_RO_TN_AT >= 0 && CGR_RO_TN_AT < D) ? CGR_RO_TN_AT : -1;
+  if (ro_at < 0) {
+    const int rc = readout_tn();
+    if (rc) return rc;
   }
   // main: ds = dzn W_n[:, F:]
   {
@@ -199,6 +213,10 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       HIP_RET(record_point(ss, side, &tn_done[l]));
       HIP_RET(tn_reduce(p, lsl, lbs, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
                         grads[CGR_PARAM_CONV_B(l)], side, 0, 0, sj));
+    }
+    if (l == ro_at) {
+      const int rc = readout_tn();
+      if (rc) return rc;
     }
     // main: dm = dpre W_l
     {

@@ -37,7 +37,16 @@ SideStreams* side_streams(hipStream_t main) {
     return nullptr;
   }
   SideStreams* s = new SideStreams();
-  if (hipStreamCreateWithFlags(&s->side, hipStreamNonBlocking) != hipSuccess) {
+  // the side stream carries only gradient-output work (weight-gradient GEMMs) and x-GEMM /
+  // transposes beside graph prep: CGR_SIDE_PRIO=1 creates it at the lowest priority so the
+  // dispatcher prefers the caller's (critical-path) stream when both have workgroups waiting
+  int least = 0, greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+#ifndef CGR_SIDE_PRIO
+#define CGR_SIDE_PRIO 0
+#endif
+  const int prio = CGR_SIDE_PRIO ? least : 0;
+  if (hipStreamCreateWithPriority(&s->side, hipStreamNonBlocking, prio) != hipSuccess) {
     set_error("cgr: hipStreamCreate failed");
     delete s;
     return nullptr;
