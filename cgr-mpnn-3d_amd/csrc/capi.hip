@@ -177,6 +177,21 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   };
   side(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N);  // readout TN runs over [xp | s] when padded
   for (int l = 0; l < (CGR_BATCH_REDUCE ? d.D : 1); ++l) side(d.H, d.H, d.E);
+  {  // the layer weight gradient may run on the register-direct kernel with its own split count
+    const int tf = tnr_layer_frags(d.H);
+    const TnrPlan q = tf == 5   ? plan_tnr<5, 5>(d.H, d.H, (int)d.E, CGR_TNR_TARGET_WGS)
+                      : tf == 4 ? plan_tnr<4, 4>(d.H, d.H, (int)d.E, CGR_TNR_TARGET_WGS)
+                                : TnrPlan{0, 0, 0, 0};
+    const size_t s = (size_t)q.splits * d.H * (size_t)((d.H + 3) & ~3);
+    const size_t bs = (size_t)q.splits * d.H;
+    if (CGR_BATCH_REDUCE) {
+      slab += (size_t)d.D * s;  // (over-allocates: both sizes counted; batching is an A/B option)
+      bslab += (size_t)d.D * bs;
+    } else {
+      slab = s > slab ? s : slab;
+      bslab = bs > bslab ? bs : bslab;
+    }
+  }
   if (d.Fe > 0) side(d.H, d.Fe, d.E);
   W.slab_elems = slab;
   W.bslab_elems = bslab;

@@ -9,6 +9,7 @@
 #include "gemm_tn.hpp"
 #include "gemm_x3.hpp"
 #include "gemm_rs.hpp"
+#include "gemm_tnr.hpp"
 
 namespace cgr {
 
@@ -75,6 +76,9 @@ inline auto with_tn_shape(int Nout, int Kout, F&& f) {
   return f(IC<4>{}, IC<4>{});
 }
 
+#ifndef CGR_TN_KT
+#define CGR_TN_KT 1  // TN k-tile depth: BE = 16 * CGR_TN_KT rows per barrier
+#endif
 #ifndef CGR_TN_TARGET_WGS
 #define CGR_TN_TARGET_WGS 1024  // floor(target / tiles) splits: 4 workgroups per CU; step-neutral vs 768 (A/B), isolated wgrad -20%
 #endif
@@ -139,6 +143,22 @@ inline hipError_t with_rs_fmax(int N, F&& f) {
   return hipErrorInvalidValue;
 }
 
+// Layer weight gradients (H x H over E rows) on the register-direct TN kernel (gemm_tnr.hpp):
+// fragments per lane 5 (H % 5 == 0: H = 400 -> 80 x 80 tiles) or 4; 0 = LDS-staged gemm_tn.
+// Lab at cfg2: 61.6 us at 20 splits vs 70 us at 40 splits for gemm_tn (and half the slab bytes).
+#ifndef CGR_TNR
+#define CGR_TNR 1
+#endif
+#ifndef CGR_TNR_TARGET_WGS
+#define CGR_TNR_TARGET_WGS 512  // 2 workgroups (8 waves) per CU: floor(512 / 25 tiles) = 20 splits
+#endif
+inline int tnr_layer_frags(int H) {
+  if (!CGR_TNR || CGR_GEMM_X3) return 0;
+  if (tnr_ok<5, 5>(H, H)) return 5;
+  if (tnr_ok<4, 4>(H, H)) return 4;
+  return 0;
+}
+
 inline TnPlan tn_plan(int Nout, int Kout, int R) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
 #if CGR_GEMM_X3
@@ -148,8 +168,8 @@ inline TnPlan tn_plan(int Nout, int Kout, int R) {
     return plan_tn2<decltype(W)::value, 1, decltype(RN)::value>(Nout, Kout, R,
                                                                  kTnTargetWorkgroups);
 #else
-    return plan_tn<decltype(W)::value, 1, decltype(RN)::value, 1>(Nout, Kout, R,
-                                                                   kTnTargetWorkgroups);
+    return plan_tn<decltype(W)::value, 1, decltype(RN)::value, CGR_TN_KT>(Nout, Kout, R,
+                                                                           kTnTargetWorkgroups);
 #endif
   });
 }
@@ -163,7 +183,7 @@ inline hipError_t launch_tn(const AL& al, const BL& bl, const TnPlan& p, float* 
 #elif CGR_TN_V2
   return launch_gemm_tn2<W, 1, RN>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
 #else
-  return launch_gemm_tn<W, 1, RN, 1>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+  return launch_gemm_tn<W, 1, RN, CGR_TN_KT>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
 #endif
 }
 

@@ -455,6 +455,9 @@ struct TNShape {
   static_assert(ACH % NT == 0, "A chunks per thread must be integral");
 };
 
+#ifndef CGR_TN_FRAG_FIRST
+#define CGR_TN_FRAG_FIRST 0
+#endif
 template <int WAVES, int RM, int RN, int KT, class AL, class BL, int PF>
 __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
     AL al, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout, int R,
@@ -548,6 +551,28 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
   auto compute = [&](int cur) {
     const float* Ab = At + cur * BE * SA;
     const float* Bb = Bt + cur * BE * SB;
+#if CGR_TN_FRAG_FIRST
+    // every fragment of the k-tile is read from LDS before the MFMAs (hipcc otherwise issues one
+    // ds_read2 pair per two MFMAs and waits lgkmcnt right before each, exposing LDS latency)
+    float av[4 * KT][RM], bv[4 * KT][RN];
+#pragma unroll
+    for (int s = 0; s < 4 * KT; ++s) {
+      const int er = 4 * s + fg;
+#pragma unroll
+      for (int i = 0; i < RM; ++i) av[s][i] = Ab[er * SA + w * 16 * RM + i * 16 + fr];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) bv[s][j] = Bb[er * SB + j * 16 + fr];
+    }
+#pragma unroll
+    for (int s = 0; s < 4 * KT; ++s)
+#pragma unroll
+      for (int i = 0; i < RM; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][i], bv[s][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, 4 * KT * (RM + RN), 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 4 * KT * RM * RN, 0);
+#else
 #pragma unroll
     for (int s = 0; s < 4 * KT; ++s) {
       const int er = 4 * s + fg;
@@ -562,6 +587,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
+#endif
     if (do_bias) {
 #pragma unroll
       for (int e = 0; e < BE; ++e) bsum += Ab[e * SA + tid];

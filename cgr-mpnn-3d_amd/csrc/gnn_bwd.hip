@@ -43,6 +43,17 @@ static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout
   });
 }
 
+// register-direct strided-fragment TN (gemm_tnr.hpp); same slab layout as tn_gemm
+template <int FA, int FB, class SA, class SB>
+static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nout, int Kout,
+                           int R, float* slab, float* bslab, bool want_bias, TnPlan* plan,
+                           hipStream_t st) {
+  const TnrPlan q = plan_tnr<FA, FB>(Nout, Kout, R, CGR_TNR_TARGET_WGS);
+  *plan = TnPlan{q.tiles_n, q.tiles_k, q.splits, q.rows_per_split};
+  ProfScope _p(name, st);
+  return launch_gemm_tnr<FA, FB>(sa, sb, q, slab, bslab, Nout, Kout, R, want_bias, st);
+}
+
 // jobs != nullptr: queue the reduction for one batched launch (CGR_BATCH_REDUCE) instead
 #ifndef CGR_RO_TN_AT
 #define CGR_RO_TN_AT -1
@@ -209,7 +220,18 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       TnPlan p;
       float *lsl, *lbs;
       side_slab(H, H, E, &lsl, &lbs);
-      HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, lsl, lbs, true, &p, side));
+      const int tf = tnr_layer_frags(H);
+      if (tf == 5) {
+        HIP_RET((tnr_gemm<5, 5>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},
+                                TnrDiff{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp}, H, H, E, lsl,
+                                lbs, true, &p, side)));
+      } else if (tf == 4) {
+        HIP_RET((tnr_gemm<4, 4>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},
+                                TnrDiff{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp}, H, H, E, lsl,
+                                lbs, true, &p, side)));
+      } else {
+        HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, lsl, lbs, true, &p, side));
+      }
       HIP_RET(record_point(ss, side, &tn_done[l]));
       HIP_RET(tn_reduce(p, lsl, lbs, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
                         grads[CGR_PARAM_CONV_B(l)], side, 0, 0, sj));
