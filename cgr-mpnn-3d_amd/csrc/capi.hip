@@ -176,6 +176,13 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     bslab += (size_t)p.splits * Nout;
   };
   side(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N);  // readout TN runs over [xp | s] when padded
+  if (!CGR_BATCH_REDUCE) {  // register-direct readout TN: its own split count
+    const int Kr = (d.F % 4 ? d.Fp : d.F) + d.H;
+    const TnrPlan q = plan_tnr<5, 4>(d.H, Kr, (int)d.N, CGR_TNR_TARGET_WGS);
+    const size_t s2 = (size_t)q.splits * d.H * (size_t)((Kr + 3) & ~3), bs2 = (size_t)q.splits * d.H;
+    slab = s2 > slab ? s2 : slab;
+    bslab = bs2 > bslab ? bs2 : bslab;
+  }
   for (int l = 0; l < (CGR_BATCH_REDUCE ? d.D : 1); ++l) side(d.H, d.H, d.E);
   {  // the layer weight gradient may run on the register-direct kernel with its own split count
     const int tf = tnr_layer_frags(d.H);
@@ -199,7 +206,14 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.bslab = b.take(4 * bslab);
   slab = 0;
   bslab = 0;
-  if (d.F > 0) acc(d.H, d.F, d.N);
+  if (d.F > 0) {
+    acc(d.H, d.F, d.N);
+    const int Fx = d.F % 4 ? d.Fp : d.F;  // register-direct node TN covers the padded columns
+    const TnrPlan q = plan_tnr<5, 4>(d.H, Fx, (int)d.N, CGR_TNR_TARGET_WGS);
+    const size_t s2 = (size_t)q.splits * d.H * (size_t)((Fx + 3) & ~3), bs2 = (size_t)q.splits * d.H;
+    slab = s2 > slab ? s2 : slab;
+    bslab = bs2 > bslab ? bs2 : bslab;
+  }
   W.slab2 = b.take(4 * (slab > 0 ? slab : 1));
   W.bslab2 = b.take(4 * (bslab > 0 ? bslab : 1));
   W.dsig_blocks = segsum_act_bwd_blocks(d.E, d.N, d.Hp);

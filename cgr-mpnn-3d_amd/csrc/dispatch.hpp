@@ -159,6 +159,23 @@ inline int tnr_layer_frags(int H) {
   return 0;
 }
 
+// x-side weight gradients (node: Gs^T x, readout: dzn^T [x | s]) on the register-direct kernel,
+// 80 x 64 tiles: H % 5 == 0, the x columns padded to 16-byte rows (Fx % 4 == 0)
+#ifndef CGR_TNR_X
+#define CGR_TNR_X 1
+#endif
+#ifndef CGR_TNR_NODE
+#define CGR_TNR_NODE 1
+#endif
+#ifndef CGR_TNR_RO
+#define CGR_TNR_RO 0  // isolated 105 -> 80 us, but the step is 2-3 % slower: beside the critical
+                      // readout NT it takes more of the CUs (same-box A/B); node TN: step -1.4 %
+#endif
+inline bool tnr_x_ok(int H, int Kx, int64_t ldx, const void* x) {
+  return CGR_TNR_X && CGR_TNR && !CGR_GEMM_X3 && tnr_ok<5, 4>(H, Kx) && ldx % 4 == 0 &&
+         ((uintptr_t)x & 15) == 0;
+}
+
 inline TnPlan tn_plan(int Nout, int Kout, int R) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
 #if CGR_GEMM_X3

@@ -87,6 +87,31 @@ struct TnrDiff {
   }
 };
 
+// [x | s] rows of the readout (GNN.py:106): value(e, c) = c < F ? x[e, c] : s[e, c - F]; F % 4 == 0
+// (x padded to 16-byte rows), so a lane's run of FB <= 4 columns never straddles the seam
+struct TnrConcat {
+  const float* x;
+  int64_t ldx;
+  const float* s;
+  int64_t lds;
+  int F;
+  struct Idx {};
+  __device__ __forceinline__ Idx idx(int) const { return Idx{}; }
+  template <int F_>
+  struct Raw {
+    float v[F_];
+  };
+  template <int F_>
+  __device__ __forceinline__ void fetch(int e, const Idx&, int c, Raw<F_>& r) const {
+    tnr_ld<F_>(c < F ? x + (int64_t)e * ldx + c : s + (int64_t)e * lds + (c - F), r.v);
+  }
+  template <int F_>
+  __device__ __forceinline__ void combine(const Raw<F_>& r, float (&v)[F_]) const {
+#pragma unroll
+    for (int i = 0; i < F_; ++i) v[i] = r.v[i];
+  }
+};
+
 struct TnrPlan {
   int tiles_n, tiles_k, splits, rows_per_split;
 };

@@ -138,7 +138,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       side_slab(H, Fp + H, N, &rsl, &rbs);
       LdPlain<4> al{dzn, Hp};
       LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
-      HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side));
+      if (CGR_TNR_RO && tnr_x_ok(H, Fp + H, Fp, fv.xp)) {
+        HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
+                                TnrConcat{fv.xp, Fp, fv.a[D], Hp, Fp}, H, Fp + H, N, rsl, rbs,
+                                true, &p, side)));
+      } else {
+        HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side));
+      }
       HIP_RET(tn_reduce(p, rsl, rbs, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
                         grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F, sj));
     } else {
@@ -146,12 +152,18 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       TnPlan p;
       float *rsl, *rbs;
       side_slab(H, F + H, N, &rsl, &rbs);
-      hipError_t e = with_vec(vx, [&](auto VX) {
-        LdPlain<4> al{dzn, Hp};
-        LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
-        return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, rsl, rbs, true, &p, side);
-      });
-      HIP_RET(e);
+      if (CGR_TNR_RO && F % 4 == 0 && tnr_x_ok(H, F + H, F, b->x)) {
+        HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
+                                TnrConcat{b->x, F, fv.a[D], Hp, F}, H, F + H, N, rsl, rbs, true,
+                                &p, side)));
+      } else {
+        hipError_t e = with_vec(vx, [&](auto VX) {
+          LdPlain<4> al{dzn, Hp};
+          LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
+          return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, rsl, rbs, true, &p, side);
+        });
+        HIP_RET(e);
+      }
       HIP_RET(tn_reduce(p, rsl, rbs, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
                         grads[CGR_PARAM_E2N_B(D)], side, 0, 0, sj));
     }
@@ -304,13 +316,21 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     const int64_t ldx = fv.xp ? d.Fp : F;
     const int vx = vec_for(xb, ldx, F);
     TnPlan p;
-    hipError_t e = with_vec(vx, [&](auto VX) {
-      LdPlain<4> al{Gs, Hp};
-      LdPlain<decltype(VX)::value> bl{xb, ldx};
-      return tn_gemm("gemm_tn_wgrad_node", al, bl, H, F, N, slab2, bslab2, Fe == 0, &p, st);
-    });
-    HIP_RET(e);
-    HIP_RET(tn_reduce(p, slab2, bslab2, H, F, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st));
+    const int Fx = fv.xp ? d.Fp : F;  // x columns the GEMM covers (pad columns are zero)
+    if (CGR_TNR_NODE && tnr_x_ok(H, Fx, ldx, xb)) {
+      HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_node", TnrRows{Gs, Hp}, TnrRows{xb, ldx}, H, Fx, N,
+                              slab2, bslab2, Fe == 0, &p, st)));
+      HIP_RET(tn_reduce(p, slab2, bslab2, H, Fx, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st, F,
+                        Fx - F));
+    } else {
+      hipError_t e = with_vec(vx, [&](auto VX) {
+        LdPlain<4> al{Gs, Hp};
+        LdPlain<decltype(VX)::value> bl{xb, ldx};
+        return tn_gemm("gemm_tn_wgrad_node", al, bl, H, F, N, slab2, bslab2, Fe == 0, &p, st);
+      });
+      HIP_RET(e);
+      HIP_RET(tn_reduce(p, slab2, bslab2, H, F, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st));
+    }
   } else if (Fe == 0) {
     HIP_RET(hipMemsetAsync(gb0, 0, sizeof(float) * H, st));
   }
