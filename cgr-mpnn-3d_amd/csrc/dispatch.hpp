@@ -43,7 +43,7 @@ inline auto with_nt_rn(int N, F&& f) {
 
 // x-GEMM k-tile depth (BK = 16 * KT) and the waves of the node-row (N-row) NT GEMMs
 #ifndef CGR_XGEMM_KT
-#define CGR_XGEMM_KT 2
+#define CGR_XGEMM_KT 1  // with interleaved loads (CGR_NT_IL) 16-deep tiles win: x-GEMM 119 -> 113 us
 #endif
 #ifndef CGR_NODE_NT_WAVES
 #define CGR_NODE_NT_WAVES 4

@@ -472,6 +472,9 @@ struct TNShape {
   static_assert(ACH % NT == 0, "A chunks per thread must be integral");
 };
 
+#ifndef CGR_TN_IL
+#define CGR_TN_IL 0  // interleaved loads in the LDS-staged TN: A/B neutral (readout TN 106 us either way)
+#endif
 #ifndef CGR_TN_FRAG_FIRST
 #define CGR_TN_FRAG_FIRST 0
 #endif
@@ -620,16 +623,36 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
       sstore(x, 0);
     }
     __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-      const int cur = t & 1;
-      const bool more = t + 1 < nt;
-      if (more) {
-        fetch(x);       // tile t+1, rows prepared during the previous iteration
-        mkrows(t + 2);  // index loads for tile t+2
+    if constexpr (CGR_TN_IL > 0) {
+      // branch-free: tiles past the split fetch in-bounds rows masked by combine (and land in the
+      // idle buffer), so the next tile's loads can be spread over this tile's MFMAs
+      for (int t = 0; t < nt; ++t) {
+        const int cur = t & 1;
+        fetch(x);
+        mkrows(t + 2);
+        compute(cur);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 * KT * (RM + RN), 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, CGR_TN_IL, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        sstore(x, cur ^ 1);
+        __syncthreads();
       }
-      compute(cur);
-      if (more) sstore(x, cur ^ 1);
-      __syncthreads();
+    } else {
+      for (int t = 0; t < nt; ++t) {
+        const int cur = t & 1;
+        const bool more = t + 1 < nt;
+        if (more) {
+          fetch(x);       // tile t+1, rows prepared during the previous iteration
+          mkrows(t + 2);  // index loads for tile t+2
+        }
+        compute(cur);
+        if (more) sstore(x, cur ^ 1);
+        __syncthreads();
+      }
     }
   } else if (nt > 0) {
     // prefetch distance 2: tile t+2 is fetched before tile t is computed and written to LDS at
