@@ -26,6 +26,14 @@ from collections import defaultdict
 
 def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
     n = name
+    if "gemm_rs_kernel" in n:
+        return "gemm_nt_layer_fwd" if "EpLayer" in n else "gemm_nt_layer_bwd"
+    if "gemm_tnr_kernel" in n:
+        if "TnrDiff" in n:
+            return "gemm_tn_wgrad_layer"
+        if "TnrConcat" in n:
+            return "gemm_tn_wgrad_readout"
+        return "gemm_tn_wgrad_node"
     if "gemm_tn_kernel" in n:
         if "LdGatherDiff" in n:
             return "gemm_tn_wgrad_layer"
