@@ -22,9 +22,25 @@
 namespace cgr {
 
 // F consecutive floats p[0 .. F-1] (4-byte aligned: gfx950 global loads need no 16-byte alignment)
+#ifndef CGR_TNR_LD
+#define CGR_TNR_LD 0  // lab: 0 = one 16-byte load (4-byte aligned) + scalars, 1 = scalars only,
+                      // 2 = two 16-byte-aligned 16-byte loads + shift (F <= 5)
+#endif
 template <int F>
 __device__ __forceinline__ void tnr_ld(const float* __restrict__ p, float (&v)[F]) {
-  if constexpr (F >= 4) {
+  if constexpr (CGR_TNR_LD == 1) {
+#pragma unroll
+    for (int i = 0; i < F; ++i) v[i] = p[i];
+  } else if constexpr (CGR_TNR_LD == 2 && F > 4) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const float4* q = reinterpret_cast<const float4*>(a & ~uintptr_t(15));
+    const int d = (int)((a >> 2) & 3);
+    const float4 u = q[0], w = q[1];
+    const float e[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < F; ++i)
+      v[i] = d == 0 ? e[i] : (d == 1 ? e[i + 1] : (d == 2 ? e[i + 2] : e[(i + 3) & 7]));
+  } else if constexpr (F >= 4) {
     float4 q;
     __builtin_memcpy(&q, p, 16);
     v[0] = q.x;
