@@ -150,8 +150,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   WorkspaceLayout W;
   Bump b;
   const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
-  W.dpre[0] = b.take(4 * E * Hp);
-  W.dpre[1] = b.take(4 * E * Hp);
+  for (int l = 0; l < (CGR_DPRE_RING ? 2 : d.D); ++l) W.dpre[l] = b.take(4 * E * Hp);
   W.dm = b.take(4 * E * Hp);
   W.dh0 = b.take(4 * E * Hp);
   W.dzn = b.take(4 * N * Hp);

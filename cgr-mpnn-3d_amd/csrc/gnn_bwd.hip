@@ -59,6 +59,16 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
 #define CGR_RO_TN_AT -1
 #endif
 
+#ifndef CGR_MAIN_FIRST
+#define CGR_MAIN_FIRST 1  // A/B: 1.283 -> 1.263 ms (the captured graph keeps the main chain on one queue)
+#endif
+#ifndef CGR_MAIN_FIRST_TAIL
+#define CGR_MAIN_FIRST_TAIL 0
+#endif
+#ifndef CGR_MAIN_FIRST_RO
+#define CGR_MAIN_FIRST_RO 0
+#endif
+
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
                             int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                             hipStream_t st, int gap_at = 0, int gap_len = 0,
@@ -81,8 +91,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   const FloatView fv = float_view(const_cast<void*>(arena), L, d);
   const WorkspaceLayout WL = workspace_layout(d);
   char* ws = static_cast<char*>(workspace);
-  float* dpre[2] = {reinterpret_cast<float*>(ws + WL.dpre[0]),
-                    reinterpret_cast<float*>(ws + WL.dpre[1])};
+  // dpre of layer l: buffer l (CGR_DPRE_RING: l & 1)
+  auto dpre = [&](int l) { return reinterpret_cast<float*>(ws + WL.dpre[CGR_DPRE_RING ? l & 1 : l]); };
   float* dm = reinterpret_cast<float*>(ws + WL.dm);
   float* dh0 = reinterpret_cast<float*>(ws + WL.dh0);
   float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
@@ -129,8 +139,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // side: dW_n = dzn^T [x | s], db_n.  Enqueued here (CGR_RO_TN_AT < 0) or after the layer
   // weight gradient of layer CGR_RO_TN_AT, so that it does not run beside the main stream's
   // readout/top-layer GEMMs, which sit on the critical path
-  auto readout_tn = [&]() -> int {
-    HIP_RET(fork_to(ss, st, side));
+  auto readout_tn = [&](hipEvent_t fork_ev) -> int {
+    if (fork_ev) HIP_RET(hipStreamWaitEvent(side, fork_ev, 0));
+    else HIP_RET(fork_to(ss, st, side));
     if (fv.xp) {  // [xp | s] with x padded to Fp: the pad columns are skipped by the reduce
       const int Fp = d.Fp;
       TnPlan p;
@@ -170,12 +181,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     return 0;
   };
   const int ro_at = (CGR_RO_TN_AT >= 0 && CGR_RO_TN_AT < D) ? CGR_RO_TN_AT : -1;
-  if (ro_at < 0) {
-    const int rc = readout_tn();
-    if (rc) return rc;
-  }
   // main: ds = dzn W_n[:, F:]
-  {
+  auto readout_nt = [&]() -> int {
     ProfScope _p("gemm_nt_readout_bwd", st);
     hipError_t e = with_nt_rn(H, [&](auto RN) {
       LdPlain<4> al{dzn, Hp};
@@ -184,6 +191,24 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       return launch_nt<CGR_NODE_NT_WAVES, 1, decltype(RN)::value, 1>(al, bl, ep, N, H, H, st);
     });
     HIP_RET(e);
+    return 0;
+  };
+  // CGR_MAIN_FIRST (see the layer loop): the main stream's NT is enqueued before the side work
+  // that forks from the same point
+  if (ro_at < 0 && CGR_MAIN_FIRST_RO && side != st) {
+    hipEvent_t fork_ev = nullptr;
+    HIP_RET(record_point(ss, st, &fork_ev));
+    int rc = readout_nt();
+    if (rc) return rc;
+    rc = readout_tn(fork_ev);
+    if (rc) return rc;
+  } else {
+    if (ro_at < 0) {
+      const int rc = readout_tn(nullptr);
+      if (rc) return rc;
+    }
+    const int rc = readout_nt();
+    if (rc) return rc;
   }
 
   // learnable-skip partial-sum slots per layer (same count for the fused and unfused kernels)
@@ -210,7 +235,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.E = E;
     la.H = H;
     la.Hp = Hp;
-    la.dpre = dpre[l & 1];
+    la.dpre = dpre(l);
     la.dh0 = dh0;
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
     return la;
@@ -223,9 +248,36 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // edge init: dpre0 overwrites dh0 in place (each element read then written by one thread)
   float* dpre0 = dh0;
   for (int l = D - 1; l >= 0; --l) {
-    float* dp = dpre[l & 1];  // written by the previous iteration's fused kernel (or just above)
-    // side: dW_l = dpre^T m_l, db_l = colsum(dpre)
-    HIP_RET(fork_to(ss, st, side));
+    float* dp = dpre(l);  // written by the previous iteration's fused kernel (or just above)
+    // main: dm = dpre W_l
+    auto layer_nt = [&]() -> int {
+      ProfScope _p("gemm_nt_layer_bwd", st);
+      hipError_t e = CGR_RS_BWD && use_rs(H, H, Hp, wT + l * HHp) ? with_rs_fmax(H, [&](auto FM) {
+        LdPlain<4> al{dp, Hp};
+        EpStore ep{dm, Hp, E, H, nullptr};
+        return launch_gemm_rs<CGR_RS_RM, decltype(FM)::value>(al, wT + l * HHp, Hp, ep, E, H, H, st);
+      }) : with_nt_layer(H, [&](auto WV, auto RN) {
+        LdPlain<4> al{dp, Hp};
+        LdPlain<4> bl{wT + l * HHp, Hp};
+        EpStore ep{dm, Hp, E, H, nullptr};
+        return launch_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H,
+                                                                            st);
+      });
+      HIP_RET(e);
+      return 0;
+    };
+    // side: dW_l = dpre^T m_l, db_l = colsum(dpre).  CGR_MAIN_FIRST: the fork point is recorded
+    // before the main stream's NT is enqueued and the side work after it (same dependencies;
+    // only the order in which a captured graph sees the two children differs)
+    hipEvent_t fork_ev = nullptr;
+    if (CGR_MAIN_FIRST && side != st) {
+      HIP_RET(record_point(ss, st, &fork_ev));
+      const int rc = layer_nt();
+      if (rc) return rc;
+      HIP_RET(hipStreamWaitEvent(side, fork_ev, 0));
+    } else {
+      HIP_RET(fork_to(ss, st, side));
+    }
     {
       LdPlain<4> al{dp, Hp};
       LdGatherDiff<false> bl{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
@@ -244,36 +296,24 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       } else {
         HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, lsl, lbs, true, &p, side));
       }
-      HIP_RET(record_point(ss, side, &tn_done[l]));
+      if (CGR_DPRE_RING) HIP_RET(record_point(ss, side, &tn_done[l]));
       HIP_RET(tn_reduce(p, lsl, lbs, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
                         grads[CGR_PARAM_CONV_B(l)], side, 0, 0, sj));
     }
     if (l == ro_at) {
-      const int rc = readout_tn();
+      const int rc = readout_tn(nullptr);
       if (rc) return rc;
     }
-    // main: dm = dpre W_l
-    {
-      ProfScope _p("gemm_nt_layer_bwd", st);
-      hipError_t e = CGR_RS_BWD && use_rs(H, H, Hp, wT + l * HHp) ? with_rs_fmax(H, [&](auto FM) {
-        LdPlain<4> al{dp, Hp};
-        EpStore ep{dm, Hp, E, H, nullptr};
-        return launch_gemm_rs<CGR_RS_RM, decltype(FM)::value>(al, wT + l * HHp, Hp, ep, E, H, H, st);
-      }) : with_nt_layer(H, [&](auto WV, auto RN) {
-        LdPlain<4> al{dp, Hp};
-        LdPlain<4> bl{wT + l * HHp, Hp};
-        EpStore ep{dm, Hp, E, H, nullptr};
-        return launch_nt<decltype(WV)::value, 1, decltype(RN)::value, 1>(al, bl, ep, E, H, H,
-                                                                            st);
-      });
-      HIP_RET(e);
+    if (!(CGR_MAIN_FIRST && side != st)) {
+      const int rc = layer_nt();
+      if (rc) return rc;
     }
     // main: da[v] = sum_{src(e) = v} dm[e], consumed in place by the layer below:
     // dh_l = da[dst] - dm[rev] -> dpre_{l-1} (or dpre0 of the edge init when l == 0)
     ProfScope _p("segsum_act_bwd", st);
     if (l > 0) {
-      // dpre[(l-1) & 1] was last read by the weight gradient of layer l+1
-      if (l + 1 <= D - 1) HIP_RET(hipStreamWaitEvent(st, tn_done[l + 1], 0));
+      // ring: dpre buffer (l-1) & 1 was last read by the weight gradient of layer l+1
+      if (CGR_DPRE_RING && l + 1 <= D - 1) HIP_RET(hipStreamWaitEvent(st, tn_done[l + 1], 0));
       HIP_RET(segsum_act_bwd(layer_args(l - 1), iv.src_list, iv.src_ptr, iv.dst_ptr, N, false,
                              st));
     } else {
@@ -293,15 +333,26 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   }
   float* gW0 = grads[CGR_PARAM_EDGE_INIT_W];
   float* gb0 = grads[CGR_PARAM_EDGE_INIT_B];
-  if (Fe > 0) {  // side: dW0[:, F:] = dpre0^T e, db0
-    HIP_RET(fork_to(ss, st, side));
-    LdPlain<4> al{dpre0, Hp};
-    LdPlain<4> bl{fv.e_s, d.Fep};
-    TnPlan p;
-    float *esl, *ebs;
-    side_slab(H, Fe, E, &esl, &ebs);
-    HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, esl, ebs, true, &p, side));
-    HIP_RET(tn_reduce(p, esl, ebs, H, Fe, gW0, F + Fe, F, gb0, side, 0, 0, sj));
+  // CGR_MAIN_FIRST_TAIL: fork point recorded here, the side work enqueued after the main tail
+  hipEvent_t tail_ev = nullptr;
+  if (CGR_MAIN_FIRST_TAIL && !CGR_BATCH_REDUCE && side != st) HIP_RET(record_point(ss, st, &tail_ev));
+  auto edge_tn = [&]() -> int {
+    if (Fe > 0) {  // side: dW0[:, F:] = dpre0^T e, db0
+      if (tail_ev) HIP_RET(hipStreamWaitEvent(side, tail_ev, 0));
+      else HIP_RET(fork_to(ss, st, side));
+      LdPlain<4> al{dpre0, Hp};
+      LdPlain<4> bl{fv.e_s, d.Fep};
+      TnPlan p;
+      float *esl, *ebs;
+      side_slab(H, Fe, E, &esl, &ebs);
+      HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, esl, ebs, true, &p, side));
+      HIP_RET(tn_reduce(p, esl, ebs, H, Fe, gW0, F + Fe, F, gb0, side, 0, 0, sj));
+    }
+    return 0;
+  };
+  if (!tail_ev) {
+    const int rc = edge_tn();
+    if (rc) return rc;
   }
   if (sj) {  // every side-stream weight gradient, one launch, at the end of the side stream
     ProfScope _p("splitk_reduce", side);
@@ -333,6 +384,10 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     }
   } else if (Fe == 0) {
     HIP_RET(hipMemsetAsync(gb0, 0, sizeof(float) * H, st));
+  }
+  if (tail_ev) {
+    const int rc = edge_tn();
+    if (rc) return rc;
   }
 
   if (d.learnable_skip) {

@@ -72,6 +72,9 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
   // (the key is computed by the first graph-prep kernel, see PrepArgs)
 
+#ifndef CGR_W0E_ON_MAIN
+#define CGR_W0E_ON_MAIN 1  // A/B: -0.4 % step (3/3 rounds)
+#endif
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
@@ -91,12 +94,15 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     ldx = d.Fp;
   }
 #endif
+  // W0[:, F:]^T for the edge init: on the x-GEMM's stream, or (CGR_W0E_ON_MAIN) ahead of graph
+  // prep on the caller's stream, which has slack until the x-GEMM's P is ready
+  hipStream_t w0e_st = CGR_W0E_ON_MAIN ? st : side;
   if (Fe > 0) {
-    ProfScope _p("weight_transpose", side);
+    ProfScope _p("weight_transpose", w0e_st);
     TransposeJobs tj{};
     tj.job[0] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
     tj.n = 1;
-    HIP_RET(transpose_batch(tj, side));
+    HIP_RET(transpose_batch(tj, w0e_st));
   }
   hipEvent_t p_ready = nullptr;  // P (and, unless split, Q) written
   if (F > 0) {

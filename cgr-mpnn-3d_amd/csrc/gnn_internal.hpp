@@ -108,9 +108,16 @@ struct ArenaLayout {
 #ifndef CGR_BATCH_REDUCE_BLOCKS
 #define CGR_BATCH_REDUCE_BLOCKS 1024
 #endif
+#ifndef CGR_DPRE_RING
+#define CGR_DPRE_RING 1  // 1: two dpre buffers reused across layers (the layer-l+1 weight gradient
+                         // must finish reading before the segmented sum of layer l overwrites:
+                         // one side->main wait per layer); 0: one buffer per layer, no such wait:
+                         // A/B 1.28 -> 1.35 ms (the graph maps the freed main-stream nodes onto
+                         // the side stream's queue)
+#endif
 struct WorkspaceLayout {
   size_t bytes;
-  size_t dpre[2], dm, dh0, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,
+  size_t dpre[CGR_MAX_DEPTH], dm, dh0, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,
       slab_elems, bslab_elems;
   int dsig_blocks;
 };
