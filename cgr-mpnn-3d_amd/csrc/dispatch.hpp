@@ -168,8 +168,8 @@ inline int tnr_layer_frags(int H) {
 #define CGR_TNR_NODE 1
 #endif
 #ifndef CGR_TNR_RO
-#define CGR_TNR_RO 0  // isolated 105 -> 80 us, but the step is 2-3 % slower: beside the critical
-                      // readout NT it takes more of the CUs (same-box A/B); node TN: step -1.4 %
+#define CGR_TNR_RO 1  // isolated 105 -> 80 us; with the main-first stream order (gnn_bwd.hip) the
+                      // step is 1.0 % faster (same-box A/B; before that order it was 2-3 % slower)
 #endif
 inline bool tnr_x_ok(int H, int Kx, int64_t ldx, const void* x) {
   return CGR_TNR_X && CGR_TNR && !CGR_GEMM_X3 && tnr_ok<5, 4>(H, Kx) && ldx % 4 == 0 &&
