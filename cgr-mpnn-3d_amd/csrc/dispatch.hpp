@@ -176,17 +176,17 @@ inline bool tnr_x_ok(int H, int Kx, int64_t ldx, const void* x) {
          ((uintptr_t)x & 15) == 0;
 }
 
-inline TnPlan tn_plan(int Nout, int Kout, int R) {
+inline TnPlan tn_plan(int Nout, int Kout, int R, int target = kTnTargetWorkgroups) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
 #if CGR_GEMM_X3
     return plan_tn_x3<decltype(W)::value, 1, decltype(RN)::value>(Nout, Kout, R,
-                                                                   kTnTargetWorkgroups);
+                                                                   target);
 #elif CGR_TN_V2
     return plan_tn2<decltype(W)::value, 1, decltype(RN)::value>(Nout, Kout, R,
-                                                                 kTnTargetWorkgroups);
+                                                                 target);
 #else
     return plan_tn<decltype(W)::value, 1, decltype(RN)::value, CGR_TN_KT>(Nout, Kout, R,
-                                                                           kTnTargetWorkgroups);
+                                                                           target);
 #endif
   });
 }

@@ -790,11 +790,16 @@ __global__ __launch_bounds__(256) void k_reduce_slabs_flat(RedJob J) {
 #define CGR_REDUCE_FLAT 0  // one thread per output, all splits in flight: serial 106 -> 97 us/step, but the step +3.5 % (A/B)
 #endif
 
+#ifndef CGR_REDUCE_FLAT_MAX_SPLITS
+#define CGR_REDUCE_FLAT_MAX_SPLITS 8  // flat form for short split counts (the grouped form leaves
+                                      // 8 - splits thread groups idle and iterates per block)
+#endif
+
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                         hipStream_t st, int gap_at, int gap_len) {
   RedJobs jobs{};
-  if (CGR_REDUCE_FLAT) {
+  if (CGR_REDUCE_FLAT || splits <= CGR_REDUCE_FLAT_MAX_SPLITS) {
     if (!add_reduce_job(jobs, slab, bslab, splits, Nout, Kout, dst, ld_dst, col_off, bias_dst,
                         gap_at, gap_len) || jobs.n == 0)
       return hipSuccess;
