@@ -72,8 +72,11 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
   // (the key is computed by the first graph-prep kernel, see PrepArgs)
 
+#ifndef CGR_WT_ON_MAIN
+#define CGR_WT_ON_MAIN 1  // A/B: -0.6 % (the readout no longer joins the side stream)
+#endif
 #ifndef CGR_W0E_ON_MAIN
-#define CGR_W0E_ON_MAIN 1  // A/B: -0.4 % step (3/3 rounds)
+#define CGR_W0E_ON_MAIN 0  // with CGR_WT_ON_MAIN: 0 (x-GEMM stream) 1.2234 ms, 1 1.2278, 2 1.2305 (A/B, 3 rounds); before it 1 was 0.4 % faster than 0
 #endif
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
@@ -94,16 +97,17 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     ldx = d.Fp;
   }
 #endif
-  // W0[:, F:]^T for the edge init: on the x-GEMM's stream, or (CGR_W0E_ON_MAIN) ahead of graph
-  // prep on the caller's stream, which has slack until the x-GEMM's P is ready
-  hipStream_t w0e_st = CGR_W0E_ON_MAIN ? st : side;
-  if (Fe > 0) {
-    ProfScope _p("weight_transpose", w0e_st);
+  // W0[:, F:]^T for the edge init: on the x-GEMM's stream (0), ahead of graph prep on the
+  // caller's stream (1), or on the caller's stream after graph prep (2)
+  auto w0e_transpose = [&](hipStream_t s) -> hipError_t {
+    if (Fe <= 0) return hipSuccess;
+    ProfScope _p("weight_transpose", s);
     TransposeJobs tj{};
     tj.job[0] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
     tj.n = 1;
-    HIP_RET(transpose_batch(tj, w0e_st));
-  }
+    return transpose_batch(tj, s);
+  };
+  if (CGR_W0E_ON_MAIN != 2) HIP_RET(w0e_transpose(CGR_W0E_ON_MAIN ? st : side));
   hipEvent_t p_ready = nullptr;  // P (and, unless split, Q) written
   if (F > 0) {
     int vb = vec_for(W0, F + Fe, F);
@@ -154,18 +158,27 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     HIP_RET(hipMemsetAsync(fv.Q, 0, sizeof(float) * (size_t)N * Hp, side));
     HIP_RET(record_point(ss, side, &p_ready));
   }
-  {  // W_l^T and W_n[:, F:]^T for the backward's NT GEMMs (arena), off the critical path
-    ProfScope _p("weight_transpose", side);
+  // W_l^T and W_n[:, F:]^T for the backward's NT GEMMs (arena), off the critical path: on the
+  // side stream after the x-GEMM (joined before the readout), or (CGR_WT_ON_MAIN, merged x-GEMM)
+  // on the caller's stream after graph prep, so that the side stream's last node is the x-GEMM
+  // the edge init waits for anyway and the forward has no second join (every cross-queue
+  // dependency in the captured graph costs 5-12 us)
+  constexpr bool wt_main = CGR_WT_ON_MAIN && !CGR_SPLIT_XGEMM;
+  auto weight_transposes = [&](hipStream_t s) -> hipError_t {
+    ProfScope _p("weight_transpose", s);
     const int64_t HHp = (int64_t)H * Hp;
     TransposeJobs tj{};
     for (int l = 0; l < D; ++l)
       tj.job[l] = TransposeJob{params[CGR_PARAM_CONV_W(l)], H, 0, fv.wT + l * HHp, Hp, H, H};
     tj.job[D] = TransposeJob{Wn, F + H, F, fv.wT + D * HHp, Hp, H, H};
     tj.n = D + 1;
-    HIP_RET(transpose_batch(tj, side));
+    return transpose_batch(tj, s);
+  };
+  hipEvent_t side_done = nullptr;
+  if (!wt_main) {
+    HIP_RET(weight_transposes(side));
+    HIP_RET(record_point(ss, side, &side_done));
   }
-  hipEvent_t side_done;
-  HIP_RET(record_point(ss, side, &side_done));
 
   // ---- main stream: graph bookkeeping, then join ----
   {
@@ -186,6 +199,8 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     HIP_RET(pad_rows(b->x, N, F, fv.xp, d.Fp, st));
   }
 #endif
+  if (CGR_W0E_ON_MAIN == 2) HIP_RET(w0e_transpose(st));
+  if (wt_main) HIP_RET(weight_transposes(st));
   HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
 
   if (Hp <= 512) {  // edge init + a_0 in one pass
@@ -235,7 +250,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
 
   // join: Q (split x-GEMM) and the backward transposes; the side stream is idle after this
-  HIP_RET(hipStreamWaitEvent(st, side_done, 0));
+  if (side_done) HIP_RET(hipStreamWaitEvent(st, side_done, 0));
 
   // readout: hn = act(s W_n[:, F:]^T + Q + b_n), s = a_D
   {
