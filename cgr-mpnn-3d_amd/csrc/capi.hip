@@ -213,6 +213,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     slab = s2 > slab ? s2 : slab;
     bslab = bs2 > bslab ? bs2 : bslab;
   }
+  if (d.Fe > 0) acc(d.H, d.Fe, d.E);  // the edge-feature TN may use slab2 (CGR_EDGE_TN_MAIN)
   W.slab2 = b.take(4 * (slab > 0 ? slab : 1));
   W.bslab2 = b.take(4 * (bslab > 0 ? bslab : 1));
   W.dsig_blocks = segsum_act_bwd_blocks(d.E, d.N, d.Hp);

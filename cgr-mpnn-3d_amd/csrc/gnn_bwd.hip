@@ -60,6 +60,9 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
 #define CGR_RO_TN_AT -1
 #endif
 
+#ifndef CGR_EDGE_TN_MAIN
+#define CGR_EDGE_TN_MAIN 0
+#endif
 #ifndef CGR_EDGE_TN_TARGET
 #define CGR_EDGE_TN_TARGET 256  // fewer splits, fewer CUs taken from the node TN beside it: A/B 1024 -> 256 -0.3 %, 128 +0.4 %, 64 +2 %
 #endif
@@ -67,10 +70,10 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
 #define CGR_MAIN_FIRST 1  // A/B: 1.283 -> 1.263 ms (the captured graph keeps the main chain on one queue)
 #endif
 #ifndef CGR_MAIN_FIRST_TAIL
-#define CGR_MAIN_FIRST_TAIL 0
+#define CGR_MAIN_FIRST_TAIL 1  // A/B: -0.8 % (1.220 -> 1.211 ms)
 #endif
 #ifndef CGR_MAIN_FIRST_RO
-#define CGR_MAIN_FIRST_RO 0
+#define CGR_MAIN_FIRST_RO 0  // A/B: +10 % (readout NT and TN both on the critical path)
 #endif
 
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
@@ -340,22 +343,33 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // CGR_MAIN_FIRST_TAIL: fork point recorded here, the side work enqueued after the main tail
   hipEvent_t tail_ev = nullptr;
   if (CGR_MAIN_FIRST_TAIL && !CGR_BATCH_REDUCE && side != st) HIP_RET(record_point(ss, st, &tail_ev));
+  // CGR_EDGE_TN_MAIN: the edge-feature TN follows the node TN on the caller's stream (own slab:
+  // slab2, free once the node reduce has run) instead of running beside it on the side stream
+  const bool edge_main = CGR_EDGE_TN_MAIN && side != st;
   auto edge_tn = [&]() -> int {
-    if (Fe > 0) {  // side: dW0[:, F:] = dpre0^T e, db0
-      if (tail_ev) HIP_RET(hipStreamWaitEvent(side, tail_ev, 0));
-      else HIP_RET(fork_to(ss, st, side));
+    if (Fe > 0) {  // dW0[:, F:] = dpre0^T e, db0
+      hipStream_t es = edge_main ? st : side;
+      if (!edge_main) {
+        if (tail_ev) HIP_RET(hipStreamWaitEvent(side, tail_ev, 0));
+        else HIP_RET(fork_to(ss, st, side));
+      }
       LdPlain<4> al{dpre0, Hp};
       LdPlain<4> bl{fv.e_s, d.Fep};
       TnPlan p;
       float *esl, *ebs;
-      side_slab(H, Fe, E, &esl, &ebs);
-      HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, esl, ebs, true, &p, side,
-                            CGR_EDGE_TN_TARGET));
-      HIP_RET(tn_reduce(p, esl, ebs, H, Fe, gW0, F + Fe, F, gb0, side, 0, 0, sj));
+      if (edge_main) {
+        esl = slab2;
+        ebs = bslab2;
+      } else {
+        side_slab(H, Fe, E, &esl, &ebs);
+      }
+      HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, esl, ebs, true, &p, es,
+                      CGR_EDGE_TN_TARGET));
+      HIP_RET(tn_reduce(p, esl, ebs, H, Fe, gW0, F + Fe, F, gb0, es, 0, 0, edge_main ? nullptr : sj));
     }
     return 0;
   };
-  if (!tail_ev) {
+  if (!tail_ev && !edge_main) {
     const int rc = edge_tn();
     if (rc) return rc;
   }
@@ -390,7 +404,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   } else if (Fe == 0) {
     HIP_RET(hipMemsetAsync(gb0, 0, sizeof(float) * H, st));
   }
-  if (tail_ev) {
+  if (tail_ev || edge_main) {
     const int rc = edge_tn();
     if (rc) return rc;
   }
