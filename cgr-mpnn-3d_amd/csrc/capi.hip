@@ -177,7 +177,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   side(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N);  // readout TN runs over [xp | s] when padded
   if (!CGR_BATCH_REDUCE) {  // register-direct readout TN: its own split count
     const int Kr = (d.F % 4 ? d.Fp : d.F) + d.H;
-    const TnrPlan q = plan_tnr<5, 4>(d.H, Kr, (int)d.N, CGR_TNR_TARGET_WGS);
+    const TnrPlan q = plan_tnr<5, 4>(d.H, Kr, (int)d.N, CGR_TNR_RO_TARGET);
     const size_t s2 = (size_t)q.splits * d.H * (size_t)((Kr + 3) & ~3), bs2 = (size_t)q.splits * d.H;
     slab = s2 > slab ? s2 : slab;
     bslab = bs2 > bslab ? bs2 : bslab;
@@ -208,7 +208,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   if (d.F > 0) {
     acc(d.H, d.F, d.N);
     const int Fx = d.F % 4 ? d.Fp : d.F;  // register-direct node TN covers the padded columns
-    const TnrPlan q = plan_tnr<5, 4>(d.H, Fx, (int)d.N, CGR_TNR_TARGET_WGS);
+    const TnrPlan q = plan_tnr<5, 4>(d.H, Fx, (int)d.N, CGR_TNR_NODE_TARGET);
     const size_t s2 = (size_t)q.splits * d.H * (size_t)((Fx + 3) & ~3), bs2 = (size_t)q.splits * d.H;
     slab = s2 > slab ? s2 : slab;
     bslab = bs2 > bslab ? bs2 : bslab;

@@ -152,6 +152,12 @@ inline hipError_t with_rs_fmax(int N, F&& f) {
 #ifndef CGR_TNR_TARGET_WGS
 #define CGR_TNR_TARGET_WGS 512  // 2 workgroups (8 waves) per CU: floor(512 / 25 tiles) = 20 splits
 #endif
+#ifndef CGR_TNR_NODE_TARGET
+#define CGR_TNR_NODE_TARGET CGR_TNR_TARGET_WGS  // node TN (Gs^T x, the backward's tail)
+#endif
+#ifndef CGR_TNR_RO_TARGET
+#define CGR_TNR_RO_TARGET 256  // readout TN (dzn^T [x | s]): 1 WG/CU, runs beside the main-stream tail; A/B +0.5 %
+#endif
 inline int tnr_layer_frags(int H) {
   if (!CGR_TNR || CGR_GEMM_X3) return 0;
   if (tnr_ok<5, 5>(H, H)) return 5;

@@ -48,8 +48,8 @@ static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout
 template <int FA, int FB, class SA, class SB>
 static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nout, int Kout,
                            int R, float* slab, float* bslab, bool want_bias, TnPlan* plan,
-                           hipStream_t st) {
-  const TnrPlan q = plan_tnr<FA, FB>(Nout, Kout, R, CGR_TNR_TARGET_WGS);
+                           hipStream_t st, int target = CGR_TNR_TARGET_WGS) {
+  const TnrPlan q = plan_tnr<FA, FB>(Nout, Kout, R, target);
   *plan = TnPlan{q.tiles_n, q.tiles_k, q.splits, q.rows_per_split};
   ProfScope _p(name, st);
   return launch_gemm_tnr<FA, FB>(sa, sb, q, slab, bslab, Nout, Kout, R, want_bias, st);
@@ -159,7 +159,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       if (CGR_TNR_RO && tnr_x_ok(H, Fp + H, Fp, fv.xp)) {
         HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
                                 TnrConcat{fv.xp, Fp, fv.a[D], Hp, Fp}, H, Fp + H, N, rsl, rbs,
-                                true, &p, side)));
+                                true, &p, side, CGR_TNR_RO_TARGET)));
       } else {
         HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side));
       }
@@ -173,7 +173,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       if (CGR_TNR_RO && F % 4 == 0 && tnr_x_ok(H, F + H, F, b->x)) {
         HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
                                 TnrConcat{b->x, F, fv.a[D], Hp, F}, H, F + H, N, rsl, rbs, true,
-                                &p, side)));
+                                &p, side, CGR_TNR_RO_TARGET)));
       } else {
         hipError_t e = with_vec(vx, [&](auto VX) {
           LdPlain<4> al{dzn, Hp};
@@ -389,7 +389,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     const int Fx = fv.xp ? d.Fp : F;  // x columns the GEMM covers (pad columns are zero)
     if (CGR_TNR_NODE && tnr_x_ok(H, Fx, ldx, xb)) {
       HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_node", TnrRows{Gs, Hp}, TnrRows{xb, ldx}, H, Fx, N,
-                              slab2, bslab2, Fe == 0, &p, st)));
+                              slab2, bslab2, Fe == 0, &p, st, CGR_TNR_NODE_TARGET)));
       HIP_RET(tn_reduce(p, slab2, bslab2, H, Fx, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st, F,
                         Fx - F));
     } else {
