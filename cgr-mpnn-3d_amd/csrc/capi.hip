@@ -82,7 +82,16 @@ ArenaLayout arena_layout(const Dims& d) {
   L.P = b.take(4 * N * Hp);
   L.Q = b.take(4 * N * Hp);
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
-  L.wT = b.take(4 * (size_t)(d.D + 1) * d.H * Hp);
+  L.wT = CGR_B3 ? kNone : b.take(4 * (size_t)(d.D + 1) * d.H * Hp);
+  if (CGR_B3) {
+    L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
+    L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
+    L.b3rob = b.take(16 * b3_img_u4(d.H, d.H));
+    for (int l = 0; l < d.D; ++l) {
+      L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
+      L.b3lb[l] = b.take(16 * b3_img_u4(d.H, d.H));
+    }
+  }
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
     L.a[l] = l <= d.D ? b.take(4 * N * Hp) : kNone;
@@ -142,7 +151,17 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.zn = (float*)at(arena, L.zn);
   f.hn = (float*)at(arena, L.hn);
   f.g = (float*)at(arena, L.g);
-  (void)d;
+  f.b3x = f.b3rof = f.b3rob = nullptr;
+  for (int l = 0; l < CGR_MAX_DEPTH; ++l) f.b3lf[l] = f.b3lb[l] = nullptr;
+  if (CGR_B3) {
+    f.b3x = at(arena, L.b3x);
+    f.b3rof = at(arena, L.b3rof);
+    f.b3rob = at(arena, L.b3rob);
+    for (int l = 0; l < d.D; ++l) {
+      f.b3lf[l] = at(arena, L.b3lf[l]);
+      f.b3lb[l] = at(arena, L.b3lb[l]);
+    }
+  }
   return f;
 }
 

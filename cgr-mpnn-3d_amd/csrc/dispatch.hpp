@@ -10,6 +10,7 @@
 #include "gemm_x3.hpp"
 #include "gemm_rs.hpp"
 #include "gemm_tnr.hpp"
+#include "gemm_b3.hpp"
 
 namespace cgr {
 

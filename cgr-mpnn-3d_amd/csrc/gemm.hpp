@@ -94,6 +94,9 @@ struct LdPlain {
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(v, rw.ok, k, K);
   }
+  // no masks (K % 4 == 0, finite data: rows past the end and k >= K read finite in-bounds
+  // elements whose products meet zero weights or are discarded by the epilogue)
+  __device__ __forceinline__ float4 combine_nm(const Raw& v) const { return v; }
   typedef float Raw1;  // single element k (column-blocked staging of the split-bf16 TN kernel)
   __device__ __forceinline__ Raw1 fetch1(const Row& rw, int k, int K) const {
     return rw.p[k < K ? k : 0];
@@ -128,6 +131,9 @@ struct LdTwoRows {
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(v, rw.ok, k, K);
   }
+  // no masks (K % 4 == 0, finite data: rows past the end and k >= K read finite in-bounds
+  // elements whose products meet zero weights or are discarded by the epilogue)
+  __device__ __forceinline__ float4 combine_nm(const Raw& v) const { return v; }
   typedef float Raw1;  // single element k (column-blocked staging of the split-bf16 TN kernel)
   __device__ __forceinline__ Raw1 fetch1(const Row& rw, int k, int K) const {
     return rw.p[k < K ? k : 0];
@@ -167,6 +173,7 @@ struct LdGatherDiff {
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(f4sub(v.a, v.h), rw.ok, k, K);
   }
+  __device__ __forceinline__ float4 combine_nm(const Raw& v) const { return f4sub(v.a, v.h); }
   struct Raw1 {
     float a, h;
   };
@@ -224,6 +231,9 @@ struct LdConcat {
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(v, rw.ok, k, K);
   }
+  // no masks (K % 4 == 0, finite data: rows past the end and k >= K read finite in-bounds
+  // elements whose products meet zero weights or are discarded by the epilogue)
+  __device__ __forceinline__ float4 combine_nm(const Raw& v) const { return v; }
   typedef float Raw1;  // single element k (column-blocked staging of the split-bf16 TN kernel)
   __device__ __forceinline__ Raw1 fetch1(const Row& rw, int k, int K) const {
     return *(k < F ? rw.px + k : (k < K ? rw.ps + (k - F) : rw.px));

@@ -191,6 +191,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // main: ds = dzn W_n[:, F:]
   auto readout_nt = [&]() -> int {
     ProfScope _p("gemm_nt_readout_bwd", st);
+    if (CGR_B3) {
+      HIP_RET(launch_b3nt(LdPlain<4>{dzn, Hp}, static_cast<const b3_u4*>(fv.b3rob),
+                          EpStore{ds, Hp, N, H, nullptr}, N, H, H, st));
+      return 0;
+    }
     hipError_t e = with_nt_rn(H, [&](auto RN) {
       LdPlain<4> al{dzn, Hp};
       LdPlain<4> bl{wT + D * HHp, Hp};
@@ -259,6 +264,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     // main: dm = dpre W_l
     auto layer_nt = [&]() -> int {
       ProfScope _p("gemm_nt_layer_bwd", st);
+      if (CGR_B3) {
+        HIP_RET(launch_b3nt(LdPlain<4>{dp, Hp}, static_cast<const b3_u4*>(fv.b3lb[l]),
+                            EpStore{dm, Hp, E, H, nullptr}, E, H, H, st));
+        return 0;
+      }
       hipError_t e = CGR_RS_BWD && use_rs(H, H, Hp, wT + l * HHp) ? with_rs_fmax(H, [&](auto FM) {
         LdPlain<4> al{dp, Hp};
         EpStore ep{dm, Hp, E, H, nullptr};

@@ -108,6 +108,25 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     return transpose_batch(tj, s);
   };
   if (CGR_W0E_ON_MAIN != 2) HIP_RET(w0e_transpose(CGR_W0E_ON_MAIN ? st : side));
+  if (CGR_B3) {  // split-bf16 weight images of every NT GEMM of this step (forward and backward)
+    ProfScope _p("weight_pack", side);
+    B3PackJobs pj{};
+    if (F > 0) {
+      const B3Cols cx = b3_cols(2 * H);
+      b3_u4* img = static_cast<b3_u4*>(fv.b3x);
+      HIP_RET(b3_pack_add(pj, B3PackJob{W0, F + Fe, 1, img, 0, H, H, F, cx.nimg, b3_nk(F)}, side));
+      HIP_RET(b3_pack_add(
+          pj, B3PackJob{Wn, F + H, 1, img, H, cx.nimg - H, H, F, cx.nimg, b3_nk(F)}, side));
+    }
+    HIP_RET(b3_pack_add(pj, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof), side));
+    HIP_RET(b3_pack_add(pj, b3_job(Wn + F, 1, F + H, H, H, fv.b3rob), side));
+    for (int l = 0; l < D; ++l) {
+      const float* Wl = params[CGR_PARAM_CONV_W(l)];
+      HIP_RET(b3_pack_add(pj, b3_job(Wl, H, 1, H, H, fv.b3lf[l]), side));
+      HIP_RET(b3_pack_add(pj, b3_job(Wl, 1, H, H, H, fv.b3lb[l]), side));
+    }
+    HIP_RET(b3_pack(pj, side));
+  }
   hipEvent_t p_ready = nullptr;  // P (and, unless split, Q) written
   if (F > 0) {
     int vb = vec_for(W0, F + Fe, F);
@@ -136,7 +155,15 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     }
     (void)vb;
 #else
-    {
+    if (CGR_B3) {
+      ProfScope _p("gemm_nt_x", side);
+      hipError_t e = with_vec(vx, [&](auto VX) {
+        LdPlain<decltype(VX)::value> al{xa, ldx};
+        EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
+        return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), ep, N, 2 * H, F, side);
+      });
+      HIP_RET(e);
+    } else {
       ProfScope _p("gemm_nt_x", side);
       hipError_t e = with_vec(vx, [&](auto VX) {
         return with_vec(vb, [&](auto VB) {
@@ -163,7 +190,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   // on the caller's stream after graph prep, so that the side stream's last node is the x-GEMM
   // the edge init waits for anyway and the forward has no second join (every cross-queue
   // dependency in the captured graph costs 5-12 us)
-  constexpr bool wt_main = CGR_WT_ON_MAIN && !CGR_SPLIT_XGEMM;
+  constexpr bool wt_main = CGR_WT_ON_MAIN && !CGR_SPLIT_XGEMM;  // (unused with CGR_B3: images)
   auto weight_transposes = [&](hipStream_t s) -> hipError_t {
     ProfScope _p("weight_transpose", s);
     const int64_t HHp = (int64_t)H * Hp;
@@ -175,7 +202,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     return transpose_batch(tj, s);
   };
   hipEvent_t side_done = nullptr;
-  if (!wt_main) {
+  if (!wt_main && !CGR_B3) {
     HIP_RET(weight_transposes(side));
     HIP_RET(record_point(ss, side, &side_done));
   }
@@ -200,7 +227,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
 #endif
   if (CGR_W0E_ON_MAIN == 2) HIP_RET(w0e_transpose(st));
-  if (wt_main) HIP_RET(weight_transposes(st));
+  if (wt_main && !CGR_B3) HIP_RET(weight_transposes(st));
   HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
 
   if (Hp <= 512) {  // edge init + a_0 in one pass
@@ -234,7 +261,8 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     {
       ProfScope _p("gemm_nt_layer_fwd", st);
       const int vw = vec_for(Wl, H, H);
-      hipError_t e = use_rs(H, H, H, Wl) ? with_rs_fmax(H, [&](auto FM) {
+      hipError_t e = CGR_B3 ? launch_b3nt(al, static_cast<const b3_u4*>(fv.b3lf[l]), ep, E, H, H, st)
+                   : use_rs(H, H, H, Wl) ? with_rs_fmax(H, [&](auto FM) {
         return launch_gemm_rs<CGR_RS_RM, decltype(FM)::value>(al, Wl, H, ep, E, H, H, st);
       }) : with_vec(vw, [&](auto VW) {
         return with_nt_layer(H, [&](auto WV, auto RN) {
@@ -257,7 +285,9 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     ProfScope _p("gemm_nt_readout_fwd", st);
     const int vw = vec_for(Wn + F, F + H, H);
     EpReadoutQ ep{bn, fv.Q, fv.hn, fv.zn, Hp, N, H, d.act};
-    hipError_t e = with_vec(vw, [&](auto VW) {
+    hipError_t e = CGR_B3 ? launch_b3nt(LdPlain<4>{fv.a[D], Hp}, static_cast<const b3_u4*>(fv.b3rof),
+                                        ep, N, H, H, st)
+                          : with_vec(vw, [&](auto VW) {
       return with_nt_rn(H, [&](auto RN) {
         LdPlain<4> al{fv.a[D], Hp};
         LdPlain<decltype(VW)::value> blw{Wn + F, F + H};

@@ -64,6 +64,13 @@ struct IndexView {
   int* node_graph;
 };
 
+// 1: every NT GEMM (x-GEMM, layer and readout, forward and backward) runs on the bf16 matrix
+// cores with three-piece split operands (gemm_b3.hpp); the forward packs the weight images once
+// per step.  0: exact fp32 MFMA kernels (gemm.hpp / gemm_rs.hpp).
+#ifndef CGR_B3
+#define CGR_B3 1
+#endif
+
 // Forward-saved float state inside the arena.
 struct FloatView {
   float* e_s;   // [E, Fep] sorted, zero padded edge_attr
@@ -79,6 +86,12 @@ struct FloatView {
   float* zn;                      // [N, Hp] readout pre-activation (non-ReLU only)
   float* hn;                      // [N, Hp] readout activation
   float* g;                       // [B, Hp] pooled graph embeddings
+  // split-bf16 weight images (CGR_B3; gemm_b3.hpp), packed by the forward's side stream:
+  void* b3x;                      // [W0[:, :F]; W_n[:, :F]]   (x-GEMM)
+  void* b3rof;                    // W_n[:, F:]                 (readout forward)
+  void* b3rob;                    // W_n[:, F:]^T               (readout backward)
+  void* b3lf[CGR_MAX_DEPTH];      // W_l                        (layer forward)
+  void* b3lb[CGR_MAX_DEPTH];      // W_l^T                      (layer backward)
 };
 
 struct Dims {
@@ -97,6 +110,7 @@ struct ArenaLayout {
       node_graph;
   size_t e_s, w0eT, P, Q, xp, wT, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,
       g;
+  size_t b3x, b3rof, b3rob, b3lf[CGR_MAX_DEPTH], b3lb[CGR_MAX_DEPTH];
 };
 
 // 1: every side-stream weight gradient gets its own split-K slab and all of them are reduced in

@@ -112,11 +112,16 @@ def _scatter_sum(vals: np.ndarray, index: np.ndarray, n: int) -> np.ndarray:
 # ----------------------------------------------------------------------------------------------
 def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str = "relu",
             learnable_skip: bool = False, num_graphs: int | None = None,
-            dropout_masks: list | None = None, dropout_ps: list | None = None):
+            dropout_masks: list | None = None, dropout_ps: list | None = None,
+            relu_masks: dict | None = None):
     """GNN.forward (GNN.py:76-110) in float64. Returns (y[B], cache).
 
     ``params`` uses the reference ``state_dict`` keys.  ``dropout_masks[l]`` (optional, 0/1 per
     element of h) + ``dropout_ps[l]`` reproduce ``F.dropout`` in train mode with a given mask.
+    ``relu_masks`` (ReLU only, optional): {"z0": [E,H], "zs": [D x [E,H]], "zn": [N,H]} boolean
+    "z > 0" decisions to use instead of the fp64 signs -- the test-side reconciliation of
+    pre-activations within rounding distance of 0, whose sign no fp32 implementation (the
+    reference's own CPU path included) shares with fp64 (tests/test_gpu_parity.py).
     """
     f8 = np.float64
     x = np.asarray(x, dtype=f8)
@@ -132,9 +137,17 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     rev = np.arange(E) ^ 1
 
     # GNN.py:85-87  h0 = act(edge_init(cat[x[row], edge_attr]))
+    rm = relu_masks if (relu_masks is not None and act == "relu") else None
+
+    def relu_or_mask(z, key, l=None):
+        if rm is None:
+            return act_fwd(z, act)
+        mk = rm[key] if l is None else rm[key][l]
+        return np.where(mk, z, 0.0)
+
     q0 = np.concatenate([x[src], ea], axis=1)
     z0 = q0 @ W0.T + b0
-    h0 = act_fwd(z0, act)
+    h0 = relu_or_mask(z0, "z0")
     hs, As, zs, ms = [h0], [], [], []
     h = h0
     for l in range(depth):
@@ -143,7 +156,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
         a = _scatter_sum(h, dst, N)  # GNN.py:134 propagate (sum at edge_index[1])
         m = a[src] - h[rev]  # GNN.py:136-141
         z = m @ Wl.T + bl + sig[l] * h0  # GNN.py:141 + GNN.py:94-97
-        hn = act_fwd(z, act)  # GNN.py:100-102
+        hn = relu_or_mask(z, "zs", l)  # GNN.py:100-102
         if dropout_masks is not None and dropout_ps is not None and dropout_ps[l] > 0:
             hn = hn * dropout_masks[l] / (1.0 - dropout_ps[l])
         As.append(a)
@@ -156,7 +169,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     bn = np.asarray(params["edge_to_node.bias"], f8)
     qn = np.concatenate([x, s], axis=1)  # GNN.py:106
     zn = qn @ Wn.T + bn
-    hnode = act_fwd(zn, act)  # GNN.py:107
+    hnode = relu_or_mask(zn, "zn")  # GNN.py:107
     if batch is None:
         g = hnode.sum(axis=0, keepdims=True)  # global_add_pool(h, None)
         gid = np.zeros(N, dtype=np.int64)
@@ -171,7 +184,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     cache = dict(x=x, ea=ea, src=src, dst=dst, rev=rev, q0=q0, z0=z0, hs=hs, As=As, ms=ms,
                  zs=zs, s=s, qn=qn, zn=zn, hnode=hnode, g=g, gid=gid, B=B, sig=sig, N=N, E=E,
                  depth=depth, act=act, learnable_skip=learnable_skip,
-                 masks=dropout_masks, ps=dropout_ps)
+                 masks=dropout_masks, ps=dropout_ps, relu_masks=rm)
     return y, cache
 
 
@@ -189,8 +202,16 @@ def backward(params: dict, cache: dict, dy: np.ndarray) -> dict:
     grads["ffn.weight"] = (dy[None, :] @ cache["g"])  # [1, H]
     grads["ffn.bias"] = np.asarray([dy.sum()])
     dg = dy[:, None] * wf  # [B, H]
+    rm = cache.get("relu_masks")
+
+    def grad_of(z, key, l=None):
+        if rm is None:
+            return act_grad(z, act)
+        mk = rm[key] if l is None else rm[key][l]
+        return mk.astype(z.dtype)
+
     dhnode = dg[cache["gid"]]  # pooling backward = gather by graph id
-    dzn = dhnode * act_grad(cache["zn"], act)
+    dzn = dhnode * grad_of(cache["zn"], "zn")
     grads["edge_to_node.weight"] = dzn.T @ cache["qn"]
     grads["edge_to_node.bias"] = dzn.sum(0)
     Wn = np.asarray(params["edge_to_node.weight"], f8)
@@ -200,9 +221,9 @@ def backward(params: dict, cache: dict, dy: np.ndarray) -> dict:
     dh0 = np.zeros_like(cache["hs"][0])
     for l in range(D - 1, -1, -1):
         z = cache["zs"][l]
-        dz = dh * act_grad(z, act)
+        dz = dh * grad_of(z, "zs", l)
         if cache["masks"] is not None and cache["ps"] is not None and cache["ps"][l] > 0:
-            dz = dh * cache["masks"][l] / (1.0 - cache["ps"][l]) * act_grad(z, act)
+            dz = dh * cache["masks"][l] / (1.0 - cache["ps"][l]) * grad_of(z, "zs", l)
         Wl = np.asarray(params[f"convs.{l}.lin.weight"], f8)
         grads[f"convs.{l}.lin.weight"] = dz.T @ cache["ms"][l]
         grads[f"convs.{l}.lin.bias"] = dz.sum(0)
@@ -213,17 +234,17 @@ def backward(params: dict, cache: dict, dy: np.ndarray) -> dict:
         da = _scatter_sum(dm, src, N)  # m = a[src] - h[rev]  ->  da = scatter_src(dm)
         dh = da[dst] - dm[rev]  # a = scatter_dst(h) ; rev is an involution
     dh0 += dh
-    dz0 = dh0 * act_grad(cache["z0"], act)
+    dz0 = dh0 * grad_of(cache["z0"], "z0")
     grads["edge_init.weight"] = dz0.T @ cache["q0"]
     grads["edge_init.bias"] = dz0.sum(0)
     return grads
 
 
 def loss_and_grads(params, x, edge_index, edge_attr, batch, y_true, depth, act="relu",
-                   learnable_skip=False, num_graphs=None):
+                   learnable_skip=False, num_graphs=None, relu_masks=None):
     """MSELoss(reduction='sum') (train.py:120) forward + backward: (loss, y_hat, grads)."""
     y, cache = forward(params, x, edge_index, edge_attr, batch, depth, act, learnable_skip,
-                       num_graphs)
+                       num_graphs, relu_masks=relu_masks)
     r = y - np.asarray(y_true, np.float64)
     loss = float((r * r).sum())
     grads = backward(params, cache, 2.0 * r)

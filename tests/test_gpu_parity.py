@@ -153,8 +153,69 @@ def _oracle_compare(b, H, D, act, skip, dev, seed=0):
     loss_o, y_o, g_o = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, D, act,
                                          skip, num_graphs=b.num_graphs)
     assert_y_close(pred.detach().cpu().numpy(), y_o)
-    for k, p in m.named_parameters():
-        assert_g_close(p.grad.cpu().numpy(), g_o[k], k)
+    grads = {k: p.grad.cpu().numpy() for k, p in m.named_parameters()}
+    if act == "relu" and not all(_g_ok(grads[k], g_o[k]) for k in grads):
+        g_o = _reconciled_relu_grads(m, data, b, sd, D, skip, grads)
+    for k, g in grads.items():
+        assert_g_close(g, g_o[k], k)
+
+
+def _g_ok(g, ref):
+    g, ref = np.asarray(g, np.float64), np.asarray(ref, np.float64)
+    return np.abs(g - ref).max() <= G_RTOL * (np.abs(ref).max() + 1e-30)
+
+
+AMBIGUOUS_Z = 1e-5  # |z| <= AMBIGUOUS_Z * max|z| of its tensor: sign within fp32 rounding reach
+
+
+def _reconciled_relu_grads(m, data, b, sd, D, skip, grads):
+    """Oracle gradients with the GPU's ReLU decisions at numerically ambiguous pre-activations.
+
+    A pre-activation within rounding distance of 0 has no well-defined fp32 sign: any fp32
+    implementation -- the reference's own PyTorch CPU path included -- can take the other branch
+    than fp64, and one flipped element moves a bias gradient (a column sum over ~15k edges) by
+    ~1e-4 of its max.  (tools/experiments: on test_stress_graphs_vs_oracle's batch a plain fp32
+    GEMM reproduces convs.3.lin.bias at 1.62e-4.)  So: read the GPU's decisions from its saved
+    activations, REQUIRE that it disagrees with fp64 only where |z| <= AMBIGUOUS_Z * max|z|, and
+    recompute the oracle with those decisions at exactly those elements.
+    """
+    F_, Fe = b.x.shape[1], b.edge_attr.shape[1]
+    H = m.hidden_sizes[0]
+    run = ArenaRun(_cfg_tuple(F_, Fe, H, D, "relu", skip), data.x, data.edge_index,
+                   data.edge_attr, data.batch, data.ptr, b.num_graphs,
+                   [p.detach() for p in m.native_parameters()])
+    torch.cuda.synchronize()
+    N, E = b.x.shape[0], b.edge_index.shape[1]
+    perm = run.ints("perm", E).long().cpu().numpy()
+
+    def unsort(t):
+        out = np.empty_like(t)
+        out[perm] = t
+        return out
+
+    gpu = {"z0": unsort(run.floats("h", E, index=0).cpu().numpy()) > 0,
+           "zs": [unsort(run.floats("h", E, index=l + 1).cpu().numpy()) > 0 for l in range(D)],
+           "zn": run.floats("hn", N).cpu().numpy() > 0}
+    _, cache = on.forward(sd, b.x, b.edge_index, b.edge_attr, b.batch, D, "relu", skip,
+                          b.num_graphs)
+    flips = 0
+
+    def reconcile(z, g, name):
+        nonlocal flips
+        amb = np.abs(z) <= AMBIGUOUS_Z * np.abs(z).max()
+        dis = g != (z > 0)
+        assert not (dis & ~amb).any(), \
+            f"{name}: {int((dis & ~amb).sum())} ReLU decisions differ at unambiguous |z|"
+        flips += int(dis.sum())
+        return np.where(amb, g, z > 0)
+
+    masks = {"z0": reconcile(cache["z0"], gpu["z0"], "z0"),
+             "zs": [reconcile(cache["zs"][l], gpu["zs"][l], f"z{l + 1}") for l in range(D)],
+             "zn": reconcile(cache["zn"], gpu["zn"], "zn")}
+    assert flips > 0, "gradient mismatch with no ambiguous ReLU decision to explain it"
+    _, _, g_o = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, D, "relu",
+                                  skip, num_graphs=b.num_graphs, relu_masks=masks)
+    return g_o
 
 
 def test_cfg2_shape_vs_oracle(cuda_device):
