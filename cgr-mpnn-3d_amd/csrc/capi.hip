@@ -201,6 +201,21 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     slab = s2 > slab ? s2 : slab;
     bslab = bs2 > bslab ? bs2 : bslab;
   }
+  auto b3acc = [&](int Nout, int Kout, int64_t R, int copies) {  // split-bf16 TN plans
+    if (!CGR_B3TN) return;
+    const TnPlan q = b3tn_tnplan(Nout, Kout, (int)R);
+    const size_t s = (size_t)q.splits * Nout * (size_t)((Kout + 3) & ~3);
+    const size_t bs = (size_t)q.splits * Nout;
+    if (CGR_BATCH_REDUCE) {
+      slab += (size_t)copies * s;  // (over-allocates, as below)
+      bslab += (size_t)copies * bs;
+    } else {
+      slab = s > slab ? s : slab;
+      bslab = bs > bslab ? bs : bslab;
+    }
+  };
+  b3acc(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N, 1);
+  b3acc(d.H, d.H, d.E, d.D);
   for (int l = 0; l < (CGR_BATCH_REDUCE ? d.D : 1); ++l) side(d.H, d.H, d.E);
   {  // the layer weight gradient may run on the register-direct kernel with its own split count
     const int tf = tnr_layer_frags(d.H);
@@ -231,6 +246,12 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     const size_t s2 = (size_t)q.splits * d.H * (size_t)((Fx + 3) & ~3), bs2 = (size_t)q.splits * d.H;
     slab = s2 > slab ? s2 : slab;
     bslab = bs2 > bslab ? bs2 : bslab;
+    if (CGR_B3TN) {
+      const TnPlan b3 = b3tn_tnplan(d.H, Fx, (int)d.N);
+      const size_t s3 = (size_t)b3.splits * d.H * (size_t)((Fx + 3) & ~3), bs3 = (size_t)b3.splits * d.H;
+      slab = s3 > slab ? s3 : slab;
+      bslab = bs3 > bslab ? bs3 : bslab;
+    }
   }
   if (d.Fe > 0) acc(d.H, d.Fe, d.E);  // the edge-feature TN may use slab2 (CGR_EDGE_TN_MAIN)
   W.slab2 = b.take(4 * (slab > 0 ? slab : 1));

@@ -183,6 +183,17 @@ inline bool tnr_x_ok(int H, int Kx, int64_t ldx, const void* x) {
          ((uintptr_t)x & 15) == 0;
 }
 
+// Weight gradients on the split-bf16 TN kernel (gemm_b3.hpp): layer (dpre^T (a[src] - h[rev])),
+// node (Gs^T x) and readout (dzn^T [x | s]) when the n side fits one workgroup (b3tn_ok).
+// Lab at cfg2 (tools/b3tn_lab): layer 50.6 us vs 60.4 us fp32 register-direct, node 42 vs 62.
+#ifndef CGR_B3TN
+#define CGR_B3TN 1
+#endif
+inline TnPlan b3tn_tnplan(int Nout, int Kout, int R) {
+  const B3TnPlan q = b3tn_plan(Nout, Kout, R);
+  return TnPlan{1, q.tiles_k, q.splits, q.rows_per_split};
+}
+
 inline TnPlan tn_plan(int Nout, int Kout, int R, int target = kTnTargetWorkgroups) {
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
 #if CGR_GEMM_X3
