@@ -84,7 +84,9 @@ ArenaLayout arena_layout(const Dims& d) {
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
   L.wT = CGR_B3 ? kNone : b.take(4 * (size_t)(d.D + 1) * d.H * Hp);
   if (CGR_B3) {
-    L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
+    // x-GEMM images: one of 2H rows, or (split x-GEMM) two of H rows back to back
+    const size_t xi = std::max(b3_img_u4(2 * d.H, d.F), 2 * b3_img_u4(d.H, d.F));
+    L.b3x = d.F > 0 ? b.take(16 * xi) : kNone;
     L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
     L.b3rob = b.take(16 * b3_img_u4(d.H, d.H));
     for (int l = 0; l < d.D; ++l) {

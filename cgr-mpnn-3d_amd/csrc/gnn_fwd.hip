@@ -18,6 +18,10 @@
 #include "profiling.hpp"
 #include "streams.hpp"
 
+#ifndef CGR_B3_SPLIT_X
+#define CGR_B3_SPLIT_X 0  // A/B: split 1.5 % slower (the Q half and the backward images packed beside the
+                          // layers slow them and the edge init more than the 30 us it takes off)
+#endif
 #ifndef CGR_SPLIT_XGEMM
 #define CGR_SPLIT_XGEMM 0
 #endif
@@ -108,27 +112,57 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     return transpose_batch(tj, s);
   };
   if (CGR_W0E_ON_MAIN != 2) HIP_RET(w0e_transpose(CGR_W0E_ON_MAIN ? st : side));
+  // split x-GEMM (CGR_B3_SPLIT_X): P = x W0[:, :F]^T first (the edge init waits for it), then
+  // Q = x W_n[:, :F]^T beside the layers (only the readout reads it), from two images in b3x
+  const bool split_x = CGR_B3 && CGR_B3_SPLIT_X && F > 0;
+  b3_u4* ximg = static_cast<b3_u4*>(fv.b3x);
+  b3_u4* ximg_q = split_x ? ximg + b3_img_u4(H, F) : nullptr;
   if (CGR_B3) {  // split-bf16 weight images of every NT GEMM of this step (forward and backward)
     ProfScope _p("weight_pack", side);
     B3PackJobs pj{};
-    if (F > 0) {
+    if (split_x) {
+      HIP_RET(b3_pack_add(pj, b3_job(W0, F + Fe, 1, H, F, ximg), side));
+      HIP_RET(b3_pack_add(pj, b3_job(Wn, F + H, 1, H, F, ximg_q), side));
+    } else if (F > 0) {
       const B3Cols cx = b3_cols(2 * H);
-      b3_u4* img = static_cast<b3_u4*>(fv.b3x);
-      HIP_RET(b3_pack_add(pj, B3PackJob{W0, F + Fe, 1, img, 0, H, H, F, cx.nimg, b3_nk(F)}, side));
+      HIP_RET(b3_pack_add(pj, B3PackJob{W0, F + Fe, 1, ximg, 0, H, H, F, cx.nimg, b3_nk(F)}, side));
       HIP_RET(b3_pack_add(
-          pj, B3PackJob{Wn, F + H, 1, img, H, cx.nimg - H, H, F, cx.nimg, b3_nk(F)}, side));
+          pj, B3PackJob{Wn, F + H, 1, ximg, H, cx.nimg - H, H, F, cx.nimg, b3_nk(F)}, side));
     }
     HIP_RET(b3_pack_add(pj, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof), side));
-    HIP_RET(b3_pack_add(pj, b3_job(Wn + F, 1, F + H, H, H, fv.b3rob), side));
-    for (int l = 0; l < D; ++l) {
-      const float* Wl = params[CGR_PARAM_CONV_W(l)];
-      HIP_RET(b3_pack_add(pj, b3_job(Wl, H, 1, H, H, fv.b3lf[l]), side));
-      HIP_RET(b3_pack_add(pj, b3_job(Wl, 1, H, H, H, fv.b3lb[l]), side));
+    for (int l = 0; l < D; ++l)
+      HIP_RET(b3_pack_add(pj, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l]), side));
+    if (!split_x) {  // backward images in the same launch
+      HIP_RET(b3_pack_add(pj, b3_job(Wn + F, 1, F + H, H, H, fv.b3rob), side));
+      for (int l = 0; l < D; ++l)
+        HIP_RET(b3_pack_add(pj, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l]), side));
     }
     HIP_RET(b3_pack(pj, side));
   }
   hipEvent_t p_ready = nullptr;  // P (and, unless split, Q) written
-  if (F > 0) {
+  hipEvent_t q_ready = nullptr;  // split x-GEMM: Q and the backward images written
+  if (split_x) {
+    const int vx = vec_for(xa, ldx, F);
+    for (int part = 0; part < 2; ++part) {
+      ProfScope _p("gemm_nt_x", side);
+      hipError_t e = with_vec(vx, [&](auto VX) {
+        LdPlain<decltype(VX)::value> al{xa, ldx};
+        EpStore ep{part == 0 ? fv.P : fv.Q, Hp, (int)N, H, nullptr};
+        return launch_b3nt(al, part == 0 ? ximg : ximg_q, ep, N, H, F, side);
+      });
+      HIP_RET(e);
+      if (part == 0) HIP_RET(record_point(ss, side, &p_ready));
+    }
+    {
+      ProfScope _p("weight_pack", side);
+      B3PackJobs pj{};
+      HIP_RET(b3_pack_add(pj, b3_job(Wn + F, 1, F + H, H, H, fv.b3rob), side));
+      for (int l = 0; l < D; ++l)
+        HIP_RET(b3_pack_add(pj, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l]), side));
+      HIP_RET(b3_pack(pj, side));
+    }
+    HIP_RET(record_point(ss, side, &q_ready));
+  } else if (F > 0) {
     int vb = vec_for(W0, F + Fe, F);
     const int vb2 = vec_for(Wn, F + H, F);
     vb = vb < vb2 ? vb : vb2;
@@ -277,8 +311,9 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
   }
 
-  // join: Q (split x-GEMM) and the backward transposes; the side stream is idle after this
+  // join: Q (split x-GEMM) and the backward transposes / images; the side stream is idle after this
   if (side_done) HIP_RET(hipStreamWaitEvent(st, side_done, 0));
+  if (q_ready) HIP_RET(hipStreamWaitEvent(st, q_ready, 0));
 
   // readout: hn = act(s W_n[:, F:]^T + Q + b_n), s = a_D
   {
