@@ -22,10 +22,11 @@ class _DMPNNConvFunction(torch.autograd.Function):
                               device=dev)
         a = torch.empty(num_nodes, H, dtype=torch.float32, device=dev)
         out = torch.empty(E, H, dtype=torch.float32, device=dev)
-        native.check(lib.cgr_dmpnn_conv_forward(
-            native.ptr(edge_index), num_nodes, E, native.ptr(h), H, native.ptr(weight),
-            native.ptr(bias), native.ptr(a), native.ptr(out), native.ptr(scratch),
-            native.stream_ptr(dev)))
+        with native.device_guard(dev):
+            native.check(lib.cgr_dmpnn_conv_forward(
+                native.ptr(edge_index), num_nodes, E, native.ptr(h), H, native.ptr(weight),
+                native.ptr(bias), native.ptr(a), native.ptr(out), native.ptr(scratch),
+                native.stream_ptr(dev)))
         ctx.save_for_backward(edge_index, h, weight, scratch)
         ctx.num_nodes = num_nodes
         return a, out
@@ -41,10 +42,11 @@ class _DMPNNConvFunction(torch.autograd.Function):
         gb = torch.empty(H, dtype=torch.float32, device=dev)
         ga = None if grad_a is None else grad_a.contiguous().float()
         go = None if grad_out is None else grad_out.contiguous().float()
-        native.check(lib.cgr_dmpnn_conv_backward(
-            native.ptr(edge_index), ctx.num_nodes, E, native.ptr(h), H, native.ptr(weight),
-            native.ptr(ga), native.ptr(go), native.ptr(gh), native.ptr(gw), native.ptr(gb),
-            native.ptr(scratch), native.stream_ptr(dev)))
+        with native.device_guard(dev):
+            native.check(lib.cgr_dmpnn_conv_backward(
+                native.ptr(edge_index), ctx.num_nodes, E, native.ptr(h), H, native.ptr(weight),
+                native.ptr(ga), native.ptr(go), native.ptr(gh), native.ptr(gw), native.ptr(gb),
+                native.ptr(scratch), native.stream_ptr(dev)))
         return None, gh, gw, gb, None
 
 

@@ -113,13 +113,14 @@ class GraphStore:
         ptr = torch.empty(B + 1, dtype=torch.int64, device=dev)
         y = torch.empty(B, dtype=torch.float32, device=dev) if self.y is not None else None
         if B:
-            native.check(self._lib.cgr_collate(
-                native.ptr(gid), B, native.ptr(self.node_ptr), native.ptr(self.edge_ptr),
-                native.ptr(self.x), self.F, native.ptr(self.edge_index),
-                int(self.edge_index.shape[1]), native.ptr(self.edge_attr), self.Fe,
-                native.ptr(self.y), native.ptr(x), native.ptr(ei), E, native.ptr(ea),
-                native.ptr(bt), native.ptr(ptr), native.ptr(y),
-                stream if stream is not None else native.stream_ptr(dev)))
+            with native.device_guard(dev):
+                native.check(self._lib.cgr_collate(
+                    native.ptr(gid), B, native.ptr(self.node_ptr), native.ptr(self.edge_ptr),
+                    native.ptr(self.x), self.F, native.ptr(self.edge_index),
+                    int(self.edge_index.shape[1]), native.ptr(self.edge_attr), self.Fe,
+                    native.ptr(self.y), native.ptr(x), native.ptr(ei), E, native.ptr(ea),
+                    native.ptr(bt), native.ptr(ptr), native.ptr(y),
+                    stream if stream is not None else native.stream_ptr(dev)))
         else:
             ptr.zero_()
         out = TorchBatch(x=x, edge_index=ei, edge_attr=ea, batch=bt, ptr=ptr, y=y)

@@ -26,10 +26,12 @@ class ArenaRun:
         self._keep = (x, edge_index, edge_attr, batch, graph_ptr, params)
         self.bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, self.B)
         self.dropout_ps, self.seed, self.training = dropout_ps, seed, training
-        native.check(lib.cgr_gnn_forward(
-            ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
-            _dropout_array(dropout_ps, self.cfg.depth), ctypes.c_uint64(seed), None, int(training),
-            native.ptr(self.arena), native.ptr(self.y), native.stream_ptr(dev)))
+        with native.device_guard(dev):
+            native.check(lib.cgr_gnn_forward(
+                ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
+                _dropout_array(dropout_ps, self.cfg.depth), ctypes.c_uint64(seed), None,
+                int(training), native.ptr(self.arena), native.ptr(self.y),
+                native.stream_ptr(dev)))
 
     def offset(self, name, index=0):
         lib = native.load()
@@ -54,9 +56,10 @@ class ArenaRun:
         ws = torch.empty(lib.cgr_gnn_workspace_bytes(ctypes.byref(self.cfg), self.N, self.E,
                                                      self.B), dtype=torch.uint8, device=dev)
         grads = [torch.empty_like(p) for p in params]
-        native.check(lib.cgr_gnn_backward(
-            ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
-            _dropout_array(self.dropout_ps, self.cfg.depth), ctypes.c_uint64(self.seed),
-            int(self.training), native.ptr(self.arena), native.ptr(dy.contiguous()),
-            _param_table(grads), native.ptr(ws), native.stream_ptr(dev)))
+        with native.device_guard(dev):
+            native.check(lib.cgr_gnn_backward(
+                ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
+                _dropout_array(self.dropout_ps, self.cfg.depth), ctypes.c_uint64(self.seed),
+                int(self.training), native.ptr(self.arena), native.ptr(dy.contiguous()),
+                _param_table(grads), native.ptr(ws), native.stream_ptr(dev)))
         return grads

@@ -71,10 +71,11 @@ class GNNFunction(torch.autograd.Function):
         bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
         ptab = _param_table(params)
         dps = _dropout_array(dropout_ps, cfg.depth)
-        native.check(lib.cgr_gnn_forward(ctypes.byref(cfg), ptab, ctypes.byref(bs), dps,
-                                         ctypes.c_uint64(seed), native.ptr(rng_counter),
-                                         int(bool(training)), native.ptr(arena), native.ptr(y),
-                                         native.stream_ptr(dev)))
+        with native.device_guard(dev):
+            native.check(lib.cgr_gnn_forward(ctypes.byref(cfg), ptab, ctypes.byref(bs), dps,
+                                             ctypes.c_uint64(seed), native.ptr(rng_counter),
+                                             int(bool(training)), native.ptr(arena),
+                                             native.ptr(y), native.stream_ptr(dev)))
         if _config.strict:
             st = read_status(arena, cfg, N, E, B)
             if st & 1:
@@ -109,11 +110,12 @@ class GNNFunction(torch.autograd.Function):
             off += n
         dy = dy.contiguous().float()
         bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
-        native.check(lib.cgr_gnn_backward(
-            ctypes.byref(cfg), _param_table(params), ctypes.byref(bs),
-            _dropout_array(ctx.dropout_ps, cfg.depth), ctypes.c_uint64(ctx.seed),
-            int(bool(ctx.training)), native.ptr(arena), native.ptr(dy), _param_table(grads),
-            native.ptr(ws), native.stream_ptr(dev)))
+        with native.device_guard(dev):
+            native.check(lib.cgr_gnn_backward(
+                ctypes.byref(cfg), _param_table(params), ctypes.byref(bs),
+                _dropout_array(ctx.dropout_ps, cfg.depth), ctypes.c_uint64(ctx.seed),
+                int(bool(ctx.training)), native.ptr(arena), native.ptr(dy), _param_table(grads),
+                native.ptr(ws), native.stream_ptr(dev)))
         hook = ctx.bucket_hook if ctx.bucket_hook is not None else _config.grad_bucket_hook
         if hook is not None:
             hook(flat)  # e.g. RCCL all-reduce of the whole bucket (cgr_mpnn_3D._amd.ddp)

@@ -143,6 +143,15 @@ def stream_ptr(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def device_guard(device):
+    """Context making ``device`` the current HIP device around a native call: the C ABI enqueues
+    on the stream it is given, but side streams, events and allocations follow the current
+    device, so a model on cuda:1 driven while cuda:0 is current must switch first."""
+    import torch
+
+    return torch.cuda.device(device)
+
+
 def profile_report() -> dict:
     """{kernel class: (launches, total_ms)} accumulated since the last cgr_profile_reset()."""
     lib = load()

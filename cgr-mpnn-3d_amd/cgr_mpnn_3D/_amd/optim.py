@@ -81,8 +81,13 @@ class FusedAdam(torch.optim.Optimizer):
                                               st["exp_avg_sq"].data_ptr(),
                                               st["max_exp_avg_sq"].data_ptr(),
                                               st["step"].data_ptr(), p.numel())
-            native.check(self._lib.cgr_adam_step(
-                tab, len(ps), float(group["lr"]), float(beta1), float(beta2),
-                float(group["eps"]), float(group["weight_decay"]), int(bool(group["amsgrad"])),
-                int(bool(group["maximize"])), native.stream_ptr(ps[0].device)))
+            dev = ps[0].device
+            if any(p.device != dev for p in ps):
+                raise RuntimeError("FusedAdam: all parameters of a group must be on one device")
+            with native.device_guard(dev):
+                native.check(self._lib.cgr_adam_step(
+                    tab, len(ps), float(group["lr"]), float(beta1), float(beta2),
+                    float(group["eps"]), float(group["weight_decay"]),
+                    int(bool(group["amsgrad"])), int(bool(group["maximize"])),
+                    native.stream_ptr(dev)))
         return loss

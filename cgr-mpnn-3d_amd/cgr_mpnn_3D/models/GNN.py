@@ -94,6 +94,20 @@ class GNN(nn.Module):
         # stay the reference's)
         self.register_buffer("_cgr_rng_counter", torch.zeros(1, dtype=torch.int64),
                              persistent=False)
+        GNN._cgr_instances += 1
+        self._cgr_instance = GNN._cgr_instances
+
+    _cgr_instances = 0  # construction order salts the dropout key (two models, distinct masks)
+
+    def _cgr_dropout_seed(self, dev) -> int:
+        """Base of the dropout key: the seed of ``dev``'s CUDA generator (what torch.manual_seed
+        sets; the reference's F.dropout draws from that generator) mixed with this model's
+        construction index.  Reading it consumes nothing, so the CPU RNG stream (DataLoader
+        shuffles, random_split) runs exactly as under the reference; the masks vary per forward
+        through the device counter the native forward advances."""
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        s = int(torch.cuda.default_generators[idx].initial_seed())
+        return (s * 0x9E3779B97F4A7C15 + self._cgr_instance * 0xBF58476D1CE4E5B9) % 2**62
 
     # -- helpers -------------------------------------------------------------------------------
     def native_parameters(self):
@@ -135,6 +149,11 @@ class GNN(nn.Module):
         drop = [float(self.dropout_ps[l]) for l in range(self.depth)]  # IndexError like GNN.py:101
 
         dev = x.device
+        if torch.is_grad_enabled() and (x.requires_grad or (
+                edge_attr is not None and edge_attr.requires_grad)):
+            raise NotImplementedError(
+                "cgr_mpnn_3D (MI355X): gradients with respect to x / edge_attr are not produced "
+                "by the native backward (parameters only); detach the inputs")
         x = x.to(dtype=torch.float32).contiguous()
         edge_index = edge_index.to(device=dev, dtype=torch.int64).contiguous()
         F_ = x.shape[1]
@@ -173,7 +192,7 @@ class GNN(nn.Module):
             if p.dtype != torch.float32 or not p.is_cuda:
                 raise RuntimeError("cgr_mpnn_3D (MI355X): parameters must be fp32 CUDA tensors")
         training = self.training and any(p > 0 for p in drop)
-        seed = int(torch.randint(0, 2**62, (1,)).item()) if training else 0
+        seed = self._cgr_dropout_seed(dev) if training else 0
         counter = self._cgr_rng_counter
         if counter.device != dev:
             counter = self._cgr_rng_counter = counter.to(dev)

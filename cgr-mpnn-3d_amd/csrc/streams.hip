@@ -22,14 +22,42 @@ bool single_stream() {
   return on;
 }
 
+// Keyed by the device of the caller's stream (the null stream: the current device).  The side
+// stream and its events are created on that device, whatever device is current.  The event ring
+// is per device and not locked: one host thread enqueues a device's forward / backward at a time
+// (the Python layer's use; two threads driving one device concurrently need their own process).
 SideStreams* side_streams(hipStream_t main) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+  if (main) {
+    hipDevice_t d = 0;
+    if (hipStreamGetDevice(main, &d) != hipSuccess) {
+      set_error("cgr: hipStreamGetDevice failed");
+      return nullptr;
+    }
+    dev = (int)d;
+  } else if (hipGetDevice(&dev) != hipSuccess) {
     set_error("cgr: hipGetDevice failed");
+    return nullptr;
+  }
+  if (dev < 0 || dev >= 64) {
+    set_error("cgr: device ordinal out of range");
     return nullptr;
   }
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_side[dev]) return g_side[dev];
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) return nullptr;
+  struct Restore {
+    int d;
+    bool on;
+    ~Restore() {
+      if (on) (void)hipSetDevice(d);
+    }
+  } restore{cur, cur != dev};
+  if (cur != dev && hipSetDevice(dev) != hipSuccess) {
+    set_error("cgr: hipSetDevice failed");
+    return nullptr;
+  }
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (main && hipStreamIsCapturing(main, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
     set_error("cgr: first native call on this device happened inside a stream capture; run one "

@@ -31,7 +31,7 @@ def test_captured_forward_redraws_dropout_mask_per_replay(cuda_device):
 
     g = torch.cuda.CUDAGraph()
     torch.manual_seed(1234)
-    seed_cap = int(torch.randint(0, 2**62, (1,)).item())  # the draw GNN.forward makes next
+    seed_cap = m._cgr_dropout_seed(torch.device(cuda_device))  # the key base GNN.forward uses
     torch.manual_seed(1234)
     with torch.no_grad(), torch.cuda.graph(g):
         y_cap = m(data)
@@ -77,7 +77,7 @@ def test_captured_training_step_backward_uses_forward_mask(cuda_device):
     torch.cuda.synchronize()
     counter0 = int(m._cgr_rng_counter.item())
     torch.manual_seed(99)
-    seed_cap = int(torch.randint(0, 2**62, (1,)).item())
+    seed_cap = m._cgr_dropout_seed(torch.device(cuda_device))
     torch.manual_seed(99)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
