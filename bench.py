@@ -30,6 +30,7 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "reactions/sec (fwd+bwd) depth=4 hidden=400 T1x batch; 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: v_mfma_f32_*_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2516.8  # 16 x the fp32 MFMA rate (MI355X_MICROARCH.md, dense)
 
 
 def log(*a):
@@ -108,6 +109,9 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("segsum_src_bwd", 1, E * H, seg_dst + i4 * E)  # Gs = segsum_src(dpre0) for dW0[:, :F]
     add("gemm_tn_wgrad_edge", 1, 2.0 * E * H * Fe, f4 * (E * H + E * Fe + H * Fe + H))
     add("gemm_tn_wgrad_node", 1, 2.0 * N * H * F, f4 * (N * H + N * F + H * F))
+    # split-bf16 weight images, once per step: fp32 weights in, three bf16 pieces out
+    nw = 2 * H * F + (2 + 2 * D) * H * H
+    add("weight_pack", 1, 0.0, (f4 + 3 * 2.0) * nw)
     return w
 
 
@@ -115,8 +119,20 @@ def mfma_bound(name):
     return name.startswith("gemm")
 
 
+# bf16 MFMA products per fp32 multiply-add in the shipped build's GEMMs (csrc/gemm_b3.hpp): NT
+# GEMMs split both operands into three bf16 pieces (six products), the layer / node / readout
+# weight gradients into two (three products); the edge-feature weight gradient (K = Fe = 14)
+# stays on the fp32 MFMA (v_mfma_f32_16x16x4_f32)
+BF16_PRODUCTS = {"gemm_nt_x": 6, "gemm_nt_layer_fwd": 6, "gemm_nt_readout_fwd": 6,
+                 "gemm_nt_layer_bwd": 6, "gemm_nt_readout_bwd": 6, "gemm_tn_wgrad_layer": 3,
+                 "gemm_tn_wgrad_node": 3, "gemm_tn_wgrad_readout": 3}
+
+
 def roofline_entry(name, work, launches, ms_total, traffic):
-    """Per-launch roofline: algorithmic work of one launch / average launch duration."""
+    """Per-launch roofline: algorithmic work of one launch / average launch duration.  For the
+    GEMMs `achieved` is the fp32 GEMM's algorithmic FLOP/s against the fp32 MFMA peak (the path's
+    dtype); `executed_bf16` restates the same launch as the bf16 matrix-core work it issues
+    (products x algorithmic FLOPs) against the dense bf16 peak."""
     t = ms_total * 1e-3 / launches
     if mfma_bound(name):
         ach = work["flops"] / t / 1e12
@@ -124,12 +140,19 @@ def roofline_entry(name, work, launches, ms_total, traffic):
     else:
         ach = work["bytes"] / t / 1e9
         peak, unit = HBM_PEAK_GBS, "GB/s"
-    return {"kernel": name, "bound": "mfma" if mfma_bound(name) else "hbm",
-            "achieved": round(ach, 3), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
-            "traffic": traffic, "algorithmic_bytes_per_launch": work["bytes"],
-            "algorithmic_flops_per_launch": work["flops"],
-            "avg_launch_us": round(t * 1e6, 3), "launches_measured": launches,
-            "timing": "HIP events on the launch stream, instrumented serial pass"}
+    out = {"kernel": name, "bound": "mfma" if mfma_bound(name) else "hbm",
+           "achieved": round(ach, 3), "peak": peak, "unit": unit, "frac": round(ach / peak, 4),
+           "traffic": traffic, "algorithmic_bytes_per_launch": work["bytes"],
+           "algorithmic_flops_per_launch": work["flops"],
+           "avg_launch_us": round(t * 1e6, 3), "launches_measured": launches,
+           "timing": "HIP events on the launch stream, instrumented serial pass"}
+    k = BF16_PRODUCTS.get(name)
+    if k:
+        eb = k * work["flops"] / t / 1e12
+        out["executed_bf16"] = {"products_per_fma": k, "achieved": round(eb, 3),
+                                "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                                "frac": round(eb / BF16_MFMA_PEAK_TFLOPS, 4)}
+    return out
 
 
 def scatter_add_roofline(edge_index, N, H, dev, reps=50):

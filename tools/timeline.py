@@ -1,9 +1,10 @@
 """Per-step kernel timeline from a rocprofv3 --kernel-trace CSV of bench.py.
 
-usage: python tools/timeline.py gpurun_out/<dir>/run_kernel_trace.csv [step_marker]
+usage: python tools/timeline.py gpurun_out/<dir>/run_kernel_trace.csv [step_marker] [k]
 
 Steps are delimited by the fused Adam kernel (k_adam: the last kernel of a training step).  For
-the last complete step it prints every kernel (queue, start offset, duration, overlap with other
+the k-th complete step from the end (default 1: the last; a bench run under rocprofv3 ends with its
+instrumented serial pass, so pick k past those steps for a graph-replayed one) it prints every kernel (queue, start offset, duration, overlap with other
 queues) and per-queue busy time, so the critical chain and the idle gaps can be read off.
 """
 import csv
@@ -30,7 +31,8 @@ def main():
     if len(ends) < 2:
         print("fewer than two step markers")
         return
-    a, b = ends[-2] + 1, ends[-1] + 1
+    k = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+    a, b = ends[-k - 1] + 1, ends[-k] + 1
     step = rows[a:b]
     t0 = step[0][0]
     t1 = max(r[1] for r in step)

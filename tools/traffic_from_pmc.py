@@ -26,6 +26,23 @@ from collections import defaultdict
 
 def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
     n = name
+    if "gemm_b3tn_kernel" in n:  # split-bf16 TN (gemm_b3.hpp)
+        if "LdGatherDiff" in n:
+            return "gemm_tn_wgrad_layer"
+        if "LdConcat" in n:
+            return "gemm_tn_wgrad_readout"
+        return "gemm_tn_wgrad_node"
+    if "gemm_b3nt_kernel" in n:  # split-bf16 NT
+        if "EpLayer" in n:
+            return "gemm_nt_layer_fwd"
+        if "EpSplit2" in n:
+            return "gemm_nt_x"
+        if "EpReadout" in n:
+            return "gemm_nt_readout_fwd"
+        if "EpStore" in n:  # E-row layer GEMM on 8-wave tiles, N-row readout on 4-wave tiles
+            return "gemm_nt_readout_bwd" if "gemm_b3nt_kernel<4," in n else "gemm_nt_layer_bwd"
+    if "k_b3_pack" in n:
+        return "weight_pack"
     if "gemm_rs_kernel" in n:
         return "gemm_nt_layer_fwd" if "EpLayer" in n else "gemm_nt_layer_bwd"
     if "gemm_tnr_kernel" in n:
