@@ -71,6 +71,9 @@ static hipError_t b3tn_gemm(const char* name, const AL& al, const BL& bl, int No
 #define CGR_RO_TN_AT -1
 #endif
 
+#ifndef CGR_NODE_REDUCE_FLAT
+#define CGR_NODE_REDUCE_FLAT 1  // the node weight gradient's reduce ends the backward's main chain
+#endif
 #ifndef CGR_EDGE_TN_MAIN
 #define CGR_EDGE_TN_MAIN 0
 #endif
@@ -90,7 +93,7 @@ static hipError_t b3tn_gemm(const char* name, const AL& al, const BL& bl, int No
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
                             int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                             hipStream_t st, int gap_at = 0, int gap_len = 0,
-                            RedJobs* jobs = nullptr) {
+                            RedJobs* jobs = nullptr, bool flat = false) {
   if (jobs)
     return add_reduce_job(*jobs, slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off,
                           bias_dst, gap_at, gap_len)
@@ -98,7 +101,7 @@ static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bsl
                : hipErrorInvalidValue;
   ProfScope _p("splitk_reduce", st);
   return reduce_slabs(slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, st,
-                      gap_at, gap_len);
+                      gap_at, gap_len, flat);
 }
 
 int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
@@ -420,7 +423,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     if (CGR_B3TN && ldx % 4 == 0 && ((uintptr_t)xb & 15) == 0 && b3tn_ok(gal, gbl, H, N)) {
       HIP_RET(b3tn_gemm("gemm_tn_wgrad_node", gal, gbl, H, Fx, N, slab2, bslab2, Fe == 0, &p, st));
       HIP_RET(tn_reduce(p, slab2, bslab2, H, Fx, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st, F,
-                        Fx - F));
+                        Fx - F, nullptr, CGR_NODE_REDUCE_FLAT));
     } else if (CGR_TNR_NODE && tnr_x_ok(H, Fx, ldx, xb)) {
       HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_node", TnrRows{Gs, Hp}, TnrRows{xb, ldx}, H, Fx, N,
                               slab2, bslab2, Fe == 0, &p, st, CGR_TNR_NODE_TARGET)));

@@ -797,9 +797,9 @@ __global__ __launch_bounds__(256) void k_reduce_slabs_flat(RedJob J) {
 
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
-                        hipStream_t st, int gap_at, int gap_len) {
+                        hipStream_t st, int gap_at, int gap_len, bool flat) {
   RedJobs jobs{};
-  if (CGR_REDUCE_FLAT || splits <= CGR_REDUCE_FLAT_MAX_SPLITS) {
+  if (flat || CGR_REDUCE_FLAT || splits <= CGR_REDUCE_FLAT_MAX_SPLITS) {
     if (!add_reduce_job(jobs, slab, bslab, splits, Nout, Kout, dst, ld_dst, col_off, bias_dst,
                         gap_at, gap_len) || jobs.n == 0)
       return hipSuccess;

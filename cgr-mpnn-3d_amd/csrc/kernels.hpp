@@ -104,9 +104,11 @@ bool add_reduce_job(RedJobs& jobs, const float* slab, const float* bslab, int sp
                     int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                     int gap_at = 0, int gap_len = 0);
 hipError_t reduce_slabs_batched(const RedJobs& jobs, int max_blocks, hipStream_t st);
+// flat: one thread per output with every split's load in flight (the critical-path tail) instead
+// of the bounded-grid grouped form that shares the GPU with the other stream
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
-                        hipStream_t st, int gap_at = 0, int gap_len = 0);
+                        hipStream_t st, int gap_at = 0, int gap_len = 0, bool flat = false);
 
 // xp[N, ldp] = x[N, F] with zero padding columns [F, ldp) (16-byte rows for the GEMM loaders)
 hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStream_t st);
