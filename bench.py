@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--config", default="cfg2", choices=["cfg1", "cfg2", "cfg4", "cfg5"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a HIP graph (1/0; -1 = auto: on for N = 1)")
+    ap.add_argument("--loss", default="fused", choices=["fused", "torch"],
+                    help="MSELoss(sum): native cgr_mse_loss (default) or torch.nn.MSELoss")
     ap.add_argument("--optimizer", default="fused", choices=["fused", "torch"],
                     help="fused: cgr FusedAdam (one native launch); torch: torch.optim.Adam")
     ap.add_argument("--dropout", type=float, default=0.02,
@@ -405,7 +407,12 @@ def main():
     else:
         opt = torch.optim.Adam(model.parameters(), lr=1e-3, amsgrad=True,
                                capturable=bool(args.graph))
-    loss_fn = torch.nn.MSELoss(reduction="sum")
+    if args.loss == "fused":
+        from cgr_mpnn_3D._amd.loss import MSELoss
+
+        loss_fn = MSELoss(reduction="sum")  # native, one launch each way (train.py:120's loss)
+    else:
+        loss_fn = torch.nn.MSELoss(reduction="sum")
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -519,7 +526,7 @@ def main():
                 "workload": f"{args.config}: CGR-MPNN-3D depth={D} hidden={H}, {B} reactions/GPU "
                             f"({c['n_atoms']} atoms, {2 * c['n_bonds']} directed edges each), "
                             f"F={F_} (78 CGR + {c['n_mace']} MACE), Fe=14, ReLU, dropout {args.dropout}; step "
-                            f"= fwd + MSELoss(sum) + bwd + grad all-reduce (N>1) + "
+                            f"= fwd + MSELoss(sum, {'native' if args.loss == 'fused' else 'torch'}) + bwd + grad all-reduce (N>1) + "
                             f"Adam(amsgrad, {'fused native' if args.optimizer == 'fused' else 'torch foreach'})"
                             + (", HIP-graph captured" if args.graph else ""),
                 "global_batch": world * B, "parallelism": f"dp{world}"},

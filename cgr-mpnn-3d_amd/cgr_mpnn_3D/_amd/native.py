@@ -91,6 +91,10 @@ SIGNATURES = [
      [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_void_p,
       c_int64, c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
       c_void_p]),
+    ("cgr_mse_loss_forward", c_int32,
+     [c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p]),
+    ("cgr_mse_loss_backward", c_int32,
+     [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_void_p, c_void_p, c_void_p]),
     ("cgr_profile_enable", c_int32, [c_int32]),
     ("cgr_profile_collect", c_int32, []),
     ("cgr_profile_reset", None, []),

@@ -18,6 +18,9 @@
 #include "profiling.hpp"
 #include "streams.hpp"
 
+#ifndef CGR_B3_PACK_MAIN
+#define CGR_B3_PACK_MAIN 1  // layer / readout weight images packed on the caller's stream
+#endif
 #ifndef CGR_B3_SPLIT_X
 #define CGR_B3_SPLIT_X 0  // A/B: split 1.5 % slower (the Q half and the backward images packed beside the
                           // layers slow them and the edge init more than the 30 us it takes off)
@@ -117,6 +120,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   const bool split_x = CGR_B3 && CGR_B3_SPLIT_X && F > 0;
   b3_u4* ximg = static_cast<b3_u4*>(fv.b3x);
   b3_u4* ximg_q = split_x ? ximg + b3_img_u4(H, F) : nullptr;
+  B3PackJobs pack_main{};
   if (CGR_B3) {  // split-bf16 weight images of every NT GEMM of this step (forward and backward)
     ProfScope _p("weight_pack", side);
     B3PackJobs pj{};
@@ -129,15 +133,25 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       HIP_RET(b3_pack_add(
           pj, B3PackJob{Wn, F + H, 1, ximg, H, cx.nimg - H, H, F, cx.nimg, b3_nk(F)}, side));
     }
-    HIP_RET(b3_pack_add(pj, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof), side));
+    // the layer / readout images: on the caller's stream ahead of graph prep (that chain has
+    // slack beside the x-GEMM chain, and the layers that read them run there), or here
+    B3PackJobs pm{};
+    hipStream_t ms = CGR_B3_PACK_MAIN ? st : side;
+    B3PackJobs& pl = CGR_B3_PACK_MAIN ? pm : pj;
+    HIP_RET(b3_pack_add(pl, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof), ms));
     for (int l = 0; l < D; ++l)
-      HIP_RET(b3_pack_add(pj, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l]), side));
+      HIP_RET(b3_pack_add(pl, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l]), ms));
     if (!split_x) {  // backward images in the same launch
-      HIP_RET(b3_pack_add(pj, b3_job(Wn + F, 1, F + H, H, H, fv.b3rob), side));
+      HIP_RET(b3_pack_add(pl, b3_job(Wn + F, 1, F + H, H, H, fv.b3rob), ms));
       for (int l = 0; l < D; ++l)
-        HIP_RET(b3_pack_add(pj, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l]), side));
+        HIP_RET(b3_pack_add(pl, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l]), ms));
     }
     HIP_RET(b3_pack(pj, side));
+    pack_main = pm;
+  }
+  if (CGR_B3 && CGR_B3_PACK_MAIN) {  // (own scope: in instrumented runs both are the same stream)
+    ProfScope _p("weight_pack", st);
+    HIP_RET(b3_pack(pack_main, st));
   }
   hipEvent_t p_ready = nullptr;  // P (and, unless split, Q) written
   hipEvent_t q_ready = nullptr;  // split x-GEMM: Q and the backward images written

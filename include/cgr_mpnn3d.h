@@ -193,6 +193,17 @@ int cgr_collate(const int64_t* graph_ids, int64_t num_ids, const int64_t* node_p
                 int64_t num_edges_out, float* edge_attr_out, int64_t* batch_out, int64_t* ptr_out,
                 float* y_out, void* stream);
 
+/* Training loss (replaces torch.nn.MSELoss(reduction="sum") of train.py:120 as trainer.py:142-143
+ * applies it; reduction_mean != 0 is MSELoss(reduction="mean")).  input, target: device [n] fp32.
+ * forward: *loss (device scalar) = sum (input - target)^2 (/ n).  backward: grad_input =
+ * 2 (input - target) grad_loss[0] (/ n), grad_target = -grad_input; either output may be NULL.
+ * One launch each, deterministic. */
+int cgr_mse_loss_forward(const float* input, const float* target, int64_t n,
+                         int32_t reduction_mean, float* loss, void* stream);
+int cgr_mse_loss_backward(const float* input, const float* target, const float* grad_loss,
+                          int64_t n, int32_t reduction_mean, float* grad_input,
+                          float* grad_target, void* stream);
+
 /* Instrumentation (no reference counterpart): per-kernel-class device time measured with HIP
  * events recorded on the launch stream around every launch of cgr_gnn_forward/_backward.
  * Off by default; do not enable while capturing a graph.  cgr_profile_collect() waits for the
