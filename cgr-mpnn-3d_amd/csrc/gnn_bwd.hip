@@ -268,7 +268,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.H = H;
     la.Hp = Hp;
     la.dpre = dpre(l);
-    la.dh0 = dh0;
+    la.dh0 = CGR_DH0_DEFER ? nullptr : dh0;
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
     return la;
   };
@@ -365,7 +365,14 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       le.E = E;
       le.H = H;
       le.Hp = Hp;
-      le.dh0 = dh0;
+      le.dh0 = CGR_DH0_DEFER ? nullptr : dh0;
+      if (CGR_DH0_DEFER) {
+        le.nl = D;
+        for (int q = 0; q < D; ++q) {
+          le.dpre_l[q] = dpre(q);
+          le.sigma_l[q] = d.learnable_skip ? params[CGR_PARAM_SKIP(D, q)] : nullptr;
+        }
+      }
       le.dpre = dpre0;
       HIP_RET(segsum_act_bwd(le, iv.src_list, iv.src_ptr, iv.dst_ptr, N, true, st));
     }

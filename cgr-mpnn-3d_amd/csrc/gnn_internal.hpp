@@ -122,13 +122,21 @@ struct ArenaLayout {
 #ifndef CGR_BATCH_REDUCE_BLOCKS
 #define CGR_BATCH_REDUCE_BLOCKS 1024
 #endif
+#ifndef CGR_DH0_DEFER
+#define CGR_DH0_DEFER 0  // 1: the skip gradient dh0 = sum_l sigma_l dpre_l is summed once by the
+                         // edge-init backward from the per-layer dpre buffers (the layer kernels
+                         // no longer read + write dh0: 2 x E x H x 4 B each); needs CGR_DPRE_RING 0.
+                         // A/B neutral: the layer kernels gain 8 us each, the edge-init backward on
+                         // the critical tail loses 28 us reading D buffers (r02 trace)
+#endif
 #ifndef CGR_DPRE_RING
-#define CGR_DPRE_RING 1  // 1: two dpre buffers reused across layers (the layer-l+1 weight gradient
+#define CGR_DPRE_RING (CGR_DH0_DEFER ? 0 : 1)  // 1: two dpre buffers reused across layers (the layer-l+1 weight gradient
                          // must finish reading before the segmented sum of layer l overwrites:
                          // one side->main wait per layer); 0: one buffer per layer, no such wait:
                          // A/B 1.28 -> 1.35 ms (the graph maps the freed main-stream nodes onto
                          // the side stream's queue)
 #endif
+static_assert(!(CGR_DH0_DEFER && CGR_DPRE_RING), "deferred dh0 needs one dpre buffer per layer");
 struct WorkspaceLayout {
   size_t bytes;
   size_t dpre[CGR_MAX_DEPTH], dm, dh0, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,

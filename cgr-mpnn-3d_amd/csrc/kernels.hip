@@ -452,13 +452,15 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
   }
   const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
   *reinterpret_cast<float4*>(a.dpre + o) = dp;
-  const float sg = a.sigma ? a.sigma[0] : 1.f;
-  float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
-  acc.x += sg * dp.x;
-  acc.y += sg * dp.y;
-  acc.z += sg * dp.z;
-  acc.w += sg * dp.w;
-  *reinterpret_cast<float4*>(a.dh0 + o) = acc;
+  if (a.dh0) {
+    const float sg = a.sigma ? a.sigma[0] : 1.f;
+    float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
+    acc.x += sg * dp.x;
+    acc.y += sg * dp.y;
+    acc.z += sg * dp.z;
+    acc.w += sg * dp.w;
+    *reinterpret_cast<float4*>(a.dh0 + o) = acc;
+  }
   if (a.dsig_part) {
     const float4 h0 = *reinterpret_cast<const float4*>(a.h0 + o);
     const float hz[4] = {h0.x, h0.y, h0.z, h0.w};
@@ -473,7 +475,21 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
 __device__ __forceinline__ void edge_init_bwd_row(const LayerBwdArgs& a, int64_t i, int n,
                                                   float4 dh) {
   const int64_t o = i * a.Hp + n;
-  float4 d = f4add(*reinterpret_cast<const float4*>(a.dh0 + o), dh);
+  float4 s0;
+  if (a.dh0) {
+    s0 = *reinterpret_cast<const float4*>(a.dh0 + o);
+  } else {  // deferred skip gradient: the layers' dpre, in the layer loop's order
+    s0 = f4zero();
+    for (int l = a.nl - 1; l >= 0; --l) {
+      const float4 dp = *reinterpret_cast<const float4*>(a.dpre_l[l] + o);
+      const float sg = a.sigma_l[l] ? a.sigma_l[l][0] : 1.f;
+      s0.x += sg * dp.x;
+      s0.y += sg * dp.y;
+      s0.z += sg * dp.z;
+      s0.w += sg * dp.w;
+    }
+  }
+  float4 d = f4add(s0, dh);
   if (a.act == ACT_RELU) {
     const float4 h = *reinterpret_cast<const float4*>(a.h0 + o);
     d.x = h.x > 0.f ? d.x : 0.f;

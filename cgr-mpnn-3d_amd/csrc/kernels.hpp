@@ -68,8 +68,13 @@ struct LayerBwdArgs {
   int64_t E;
   int H, Hp;
   float* dpre;
-  float* dh0;         // written (first) or accumulated
+  float* dh0;         // written (first) or accumulated; nullptr: not accumulated (deferred)
   float* dsig_part;   // [gridDim] partial sums of dpre*h0 (nullable)
+  // edge init with deferred dh0: dh0 = sum_{l = nl-1 .. 0} sigma_l dpre_l, summed in the order
+  // the per-layer accumulation would have used (bitwise the same)
+  int nl;
+  const float* dpre_l[32];
+  const float* sigma_l[32];
 };
 // nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
 hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);
