@@ -13,7 +13,7 @@ from .functional import _batch_struct, _dropout_array, _param_table, make_config
 
 class ArenaRun:
     def __init__(self, cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, params,
-                 dropout_ps=None, seed=0, training=False):
+                 dropout_ps=None, seed=0, training=False, prepare_backward=True):
         lib = native.load()
         self.cfg = make_config(*cfg_tuple)
         self.N, self.E, self.B = int(x.shape[0]), int(edge_index.shape[1]), int(num_graphs)
@@ -26,11 +26,14 @@ class ArenaRun:
         self._keep = (x, edge_index, edge_attr, batch, graph_ptr, params)
         self.bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, self.B)
         self.dropout_ps, self.seed, self.training = dropout_ps, seed, training
+        # prepared for the backward (this helper runs it), as a training step's forward is
+        self.flags = (native.TRAIN_DROPOUT if training else 0) | (
+            native.TRAIN_FOR_BACKWARD if prepare_backward else 0)
         with native.device_guard(dev):
             native.check(lib.cgr_gnn_forward(
                 ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
                 _dropout_array(dropout_ps, self.cfg.depth), ctypes.c_uint64(seed), None,
-                int(training), native.ptr(self.arena), native.ptr(self.y),
+                self.flags, native.ptr(self.arena), native.ptr(self.y),
                 native.stream_ptr(dev)))
 
     def offset(self, name, index=0):
@@ -60,6 +63,6 @@ class ArenaRun:
             native.check(lib.cgr_gnn_backward(
                 ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
                 _dropout_array(self.dropout_ps, self.cfg.depth), ctypes.c_uint64(self.seed),
-                int(self.training), native.ptr(self.arena), native.ptr(dy.contiguous()),
+                self.flags, native.ptr(self.arena), native.ptr(dy.contiguous()),
                 _param_table(grads), native.ptr(ws), native.stream_ptr(dev)))
         return grads

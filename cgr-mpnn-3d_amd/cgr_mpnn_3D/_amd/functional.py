@@ -71,10 +71,14 @@ class GNNFunction(torch.autograd.Function):
         bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
         ptab = _param_table(params)
         dps = _dropout_array(dropout_ps, cfg.depth)
+        # CGR_TRAIN_DROPOUT | CGR_TRAIN_FOR_BACKWARD (include/cgr_mpnn3d.h): the backward's
+        # weight-gradient operands are prepared only when a parameter gradient is wanted
+        flags = (native.TRAIN_DROPOUT if training else 0) | (
+            native.TRAIN_FOR_BACKWARD if any(ctx.needs_input_grad[12:]) else 0)
         with native.device_guard(dev):
             native.check(lib.cgr_gnn_forward(ctypes.byref(cfg), ptab, ctypes.byref(bs), dps,
                                              ctypes.c_uint64(seed), native.ptr(rng_counter),
-                                             int(bool(training)), native.ptr(arena),
+                                             flags, native.ptr(arena),
                                              native.ptr(y), native.stream_ptr(dev)))
         if _config.strict:
             st = read_status(arena, cfg, N, E, B)
@@ -87,6 +91,7 @@ class GNNFunction(torch.autograd.Function):
         ctx.dropout_ps = dropout_ps
         ctx.seed = seed
         ctx.training = training
+        ctx.flags = flags
         ctx.bucket_hook = bucket_hook
         ctx.save_for_backward(x, edge_index, edge_attr, batch, graph_ptr, arena, *params)
         return y
@@ -114,7 +119,7 @@ class GNNFunction(torch.autograd.Function):
             native.check(lib.cgr_gnn_backward(
                 ctypes.byref(cfg), _param_table(params), ctypes.byref(bs),
                 _dropout_array(ctx.dropout_ps, cfg.depth), ctypes.c_uint64(ctx.seed),
-                int(bool(ctx.training)), native.ptr(arena), native.ptr(dy), _param_table(grads),
+                ctx.flags, native.ptr(arena), native.ptr(dy), _param_table(grads),
                 native.ptr(ws), native.stream_ptr(dev)))
         hook = ctx.bucket_hook if ctx.bucket_hook is not None else _config.grad_bucket_hook
         if hook is not None:

@@ -16,6 +16,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CGR_MPNN3D_LIB", os.path.join(_HERE, "lib", _LIB_NAME))
 
 ABI_VERSION = 2
+TRAIN_DROPOUT, TRAIN_FOR_BACKWARD = 1, 2  # cgr_gnn_forward / _backward `training` bits
 MAX_DEPTH = 32
 ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
 

@@ -93,6 +93,13 @@ ArenaLayout arena_layout(const Dims& d) {
       L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
       L.b3lb[l] = b.take(16 * b3_img_u4(d.H, d.H));
     }
+    if (CGR_B3TP) {
+      const size_t pb = 2 * (size_t)b3tp_rows(d.E) * (size_t)b3tp_layer_ld(d.H);
+      for (int l = 0; l < d.D; ++l) {
+        L.mhi[l] = b.take(pb);
+        L.mlo[l] = b.take(pb);
+      }
+    }
   }
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
@@ -155,6 +162,8 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.g = (float*)at(arena, L.g);
   f.b3x = f.b3rof = f.b3rob = nullptr;
   for (int l = 0; l < CGR_MAX_DEPTH; ++l) f.b3lf[l] = f.b3lb[l] = nullptr;
+  for (int l = 0; l < CGR_MAX_DEPTH; ++l) f.mhi[l] = f.mlo[l] = nullptr;
+  f.mld = b3tp_layer_ld(d.H);
   if (CGR_B3) {
     f.b3x = at(arena, L.b3x);
     f.b3rof = at(arena, L.b3rof);
@@ -162,6 +171,10 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
     for (int l = 0; l < d.D; ++l) {
       f.b3lf[l] = at(arena, L.b3lf[l]);
       f.b3lb[l] = at(arena, L.b3lb[l]);
+      if (CGR_B3TP) {
+        f.mhi[l] = static_cast<uint16_t*>(at(arena, L.mhi[l]));
+        f.mlo[l] = static_cast<uint16_t*>(at(arena, L.mlo[l]));
+      }
     }
   }
   return f;
@@ -172,6 +185,14 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   Bump b;
   const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
   for (int l = 0; l < (CGR_DPRE_RING ? 2 : d.D); ++l) W.dpre[l] = b.take(4 * E * Hp);
+  for (int l = 0; l < CGR_MAX_DEPTH; ++l) W.dphi[l] = W.dplo[l] = (size_t)-1;
+  if (CGR_B3 && CGR_B3TP) {
+    const size_t pb = 2 * (size_t)b3tp_rows(d.E) * (size_t)b3tp_layer_ld(d.H);
+    for (int l = 0; l < (CGR_DPRE_RING ? 2 : d.D); ++l) {
+      W.dphi[l] = b.take(pb);
+      W.dplo[l] = b.take(pb);
+    }
+  }
   W.dm = b.take(4 * E * Hp);
   W.dh0 = b.take(4 * E * Hp);
   W.dzn = b.take(4 * N * Hp);
@@ -218,6 +239,17 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   };
   b3acc(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N, 1);
   b3acc(d.H, d.H, d.E, d.D);
+  if (CGR_B3 && CGR_B3TP) {  // plane TN plans of the layer weight gradients
+    const B3TpPlan q = b3tp_plan(d.H, d.H, (int)d.E);
+    const size_t s = (size_t)q.splits * d.H * (size_t)((d.H + 3) & ~3), bs = (size_t)q.splits * d.H;
+    if (CGR_BATCH_REDUCE) {
+      slab += (size_t)d.D * s;
+      bslab += (size_t)d.D * bs;
+    } else {
+      slab = s > slab ? s : slab;
+      bslab = bs > bslab ? bs : bslab;
+    }
+  }
   for (int l = 0; l < (CGR_BATCH_REDUCE ? d.D : 1); ++l) side(d.H, d.H, d.E);
   {  // the layer weight gradient may run on the register-direct kernel with its own split count
     const int tf = tnr_layer_frags(d.H);

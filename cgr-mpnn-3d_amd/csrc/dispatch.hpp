@@ -11,6 +11,7 @@
 #include "gemm_rs.hpp"
 #include "gemm_tnr.hpp"
 #include "gemm_b3.hpp"
+#include "gemm_b3tp.hpp"
 
 namespace cgr {
 

@@ -209,10 +209,27 @@ __device__ unsigned long long* b3_stamps;  // lab: [block][wave][4] s_memrealtim
 //   Column groups are processed in pairs (CGR_B3_JPAIR): the six-term chains of two groups
 //   alternate, two independent accumulators in flight.
 //   Staging past the end writes a buffer nobody reads any more (unconditional, branch-free).
-template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP>
+// Optional by-product of an NT GEMM: its A operand as two row-major bf16 planes (hi, lo: the
+// split's first two pieces, exactly what the weight-gradient TN of gemm_b3tp.hpp multiplies), for
+// rows [0, round_up(M, 32)) (rows >= M written as zeros) and the k steps' columns.  Column tile tn
+// writes the k steps ks with ks % tiles_n == tn (each A element is loaded by every column tile).
+struct B3NoPlanes {
+  static constexpr bool on = false;
+  uint16_t* hi;
+  uint16_t* lo;
+  int64_t ld;
+};
+struct B3PlaneOut {
+  static constexpr bool on = true;
+  uint16_t* hi;
+  uint16_t* lo;
+  int64_t ld;  // >= nk * 32
+};
+
+template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP, class PO = B3NoPlanes>
 __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u4* __restrict__ Bimg,
                                                                int nimg, EP ep, int M, int N,
-                                                               int K, int tiles_n) {
+                                                               int K, int tiles_n, PO po) {
   using S = B3NtShape<WAVES, RF, NF>;
   constexpr int NT = S::NT, BM = S::BM, BN = S::BN, BU4 = S::BU4, BPT = S::BPT;
   extern __shared__ b3_u4 b3_lds[];
@@ -253,6 +270,20 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       }
       const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
       b3_split8<3>(f, af[i]);
+      if constexpr (PO::on) {
+        const int row = m0 + (w * RF + i) * 16 + fr;
+        if (ks % tiles_n == tn && row < ((M + 31) & ~31) && ks < nk) {
+          const bool live = row < M;
+          const uint32_t z = 0;
+          typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+          const int64_t o = (int64_t)row * po.ld + ks * B3_BK + 4 * fg;
+          const b3_u4 h = af[i][0], l = af[i][1];
+          *reinterpret_cast<u2*>(po.hi + o) = live ? u2{h.x, h.y} : u2{z, z};
+          *reinterpret_cast<u2*>(po.hi + o + 16) = live ? u2{h.z, h.w} : u2{z, z};
+          *reinterpret_cast<u2*>(po.lo + o) = live ? u2{l.x, l.y} : u2{z, z};
+          *reinterpret_cast<u2*>(po.lo + o + 16) = live ? u2{l.z, l.w} : u2{z, z};
+        }
+      }
     }
   };
   // ---- B: the tile's column block of one (ks, piece) plane is BN * 4 contiguous b3_u4 ----
@@ -444,11 +475,11 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   B3_STAMP(3)
 }
 
-template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP>
+template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP, class PO = B3NoPlanes>
 inline hipError_t launch_b3nt_t(const AL& al, const b3_u4* Bimg, int nimg, const EP& ep, int M,
-                                int N, int K, int tiles_n, hipStream_t st) {
+                                int N, int K, int tiles_n, hipStream_t st, const PO& po = PO{}) {
   using S = B3NtShape<WAVES, RF, NF>;
-  auto kern = gemm_b3nt_kernel<WAVES, RF, NF, NOMASK, AL, EP>;
+  auto kern = gemm_b3nt_kernel<WAVES, RF, NF, NOMASK, AL, EP, PO>;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -458,7 +489,7 @@ inline hipError_t launch_b3nt_t(const AL& al, const b3_u4* Bimg, int nimg, const
   }
   const int tm = (M + S::BM - 1) / S::BM;
   hipLaunchKernelGGL(kern, dim3(tm * tiles_n), dim3(WAVES * 64), S::LDS_BYTES, st, al, Bimg, nimg,
-                     ep, M, N, K, tiles_n);
+                     ep, M, N, K, tiles_n, po);
   return hipGetLastError();
 }
 
@@ -473,9 +504,9 @@ inline int b3nt_waves(int M, int N) {
 }
 
 // C = A B^T with B given as its image (b3_pack of the same N, K).  M, N, K > 0.
-template <class AL, class EP>
+template <class AL, class EP, class PO = B3NoPlanes>
 inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int M, int N, int K,
-                              hipStream_t st) {
+                              hipStream_t st, const PO& po = PO{}) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const B3Cols c = b3_cols(N);
   const bool w8 = b3nt_waves(M, N) == 8;
@@ -488,10 +519,10 @@ inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int
 #endif
     constexpr int W8 = 8 / CGR_B3_RF;
     if (K % 4 == 0)
-      return w8 ? launch_b3nt_t<W8, CGR_B3_RF, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st)
-                : launch_b3nt_t<4, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
-    return w8 ? launch_b3nt_t<W8, CGR_B3_RF, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st)
-              : launch_b3nt_t<4, 1, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
+      return w8 ? launch_b3nt_t<W8, CGR_B3_RF, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po)
+                : launch_b3nt_t<4, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po);
+    return w8 ? launch_b3nt_t<W8, CGR_B3_RF, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po)
+              : launch_b3nt_t<4, 1, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po);
   };
   switch (c.nf) {
     case 1: return go(std::integral_constant<int, 1>{});

@@ -114,6 +114,16 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   char* ws = static_cast<char*>(workspace);
   // dpre of layer l: buffer l (CGR_DPRE_RING: l & 1)
   auto dpre = [&](int l) { return reinterpret_cast<float*>(ws + WL.dpre[CGR_DPRE_RING ? l & 1 : l]); };
+  // weight-gradient operands as bf16 planes: the forward wrote the messages' (arena), the
+  // activation backward writes dpre's (same ring as dpre)
+  const bool planes = CGR_B3 && CGR_B3TP && (training & CGR_TRAIN_FOR_BACKWARD) && d.D > 0 &&
+                      fv.mhi[0] != nullptr;
+  auto dphi = [&](int l) {
+    return reinterpret_cast<uint16_t*>(ws + WL.dphi[CGR_DPRE_RING ? l & 1 : l]);
+  };
+  auto dplo = [&](int l) {
+    return reinterpret_cast<uint16_t*>(ws + WL.dplo[CGR_DPRE_RING ? l & 1 : l]);
+  };
   float* dm = reinterpret_cast<float*>(ws + WL.dm);
   float* dh0 = reinterpret_cast<float*>(ws + WL.dh0);
   float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
@@ -149,6 +159,14 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
   hipStream_t side = (prof_enabled() || single_stream()) ? st : ss->side;
 
+  // rows [E, round_up(E, 32)) of the dpre planes are zero (the plane TN reads whole 32-row steps)
+  if (planes && b3tp_rows(E) > E) {
+    const size_t pad = (size_t)(b3tp_rows(E) - E) * (size_t)fv.mld * 2;
+    for (int r = 0; r < (CGR_DPRE_RING ? (D < 2 ? D : 2) : D); ++r) {
+      HIP_RET(hipMemsetAsync(dphi(r) + (int64_t)E * fv.mld, 0, pad, st));
+      HIP_RET(hipMemsetAsync(dplo(r) + (int64_t)E * fv.mld, 0, pad, st));
+    }
+  }
   // head + readout
   {
     ProfScope _p("head_readout_bwd", st);
@@ -268,6 +286,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.H = H;
     la.Hp = Hp;
     la.dpre = dpre(l);
+    la.dphi = planes ? dphi(l) : nullptr;
+    la.dplo = planes ? dplo(l) : nullptr;
+    la.dpld = fv.mld;
     la.dh0 = CGR_DH0_DEFER ? nullptr : dh0;
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
     return la;
@@ -322,7 +343,14 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       float *lsl, *lbs;
       side_slab(H, H, E, &lsl, &lbs);
       const int tf = tnr_layer_frags(H);
-      if (CGR_B3TN && b3tn_ok(al, bl, H, E)) {
+      const B3TpPlan tq = b3tp_plan(H, H, E);
+      const B3Planes pa{planes ? dphi(l) : nullptr, planes ? dplo(l) : nullptr, fv.mld};
+      const B3Planes pm{fv.mhi[l], fv.mlo[l], fv.mld};
+      if (planes && b3tp_ok(pa, pm, Hp, tq)) {
+        ProfScope _pt("gemm_tn_wgrad_layer", side);
+        p = TnPlan{tq.tiles_n, tq.tiles_k, tq.splits, tq.rows_per_split};
+        HIP_RET(launch_b3tp(pa, pm, dp, Hp, tq, lsl, lbs, H, H, E, true, side));
+      } else if (CGR_B3TN && b3tn_ok(al, bl, H, E)) {
         HIP_RET(b3tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, lsl, lbs, true, &p, side));
       } else if (tf == 5) {
         HIP_RET((tnr_gemm<5, 5>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},

@@ -38,7 +38,7 @@ static void dropout_consts(const float* dropout_p, int training, int l, uint32_t
                            float* scale) {
   *thresh = 0;
   *scale = 1.f;
-  if (!training || dropout_p == nullptr) return;
+  if (!(training & CGR_TRAIN_DROPOUT) || dropout_p == nullptr) return;
   const double p = dropout_p[l];
   if (p <= 0.0) return;
   if (p >= 1.0) {
@@ -83,7 +83,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
 #define CGR_WT_ON_MAIN 1  // A/B: -0.6 % (the readout no longer joins the side stream)
 #endif
 #ifndef CGR_W0E_ON_MAIN
-#define CGR_W0E_ON_MAIN 0  // with CGR_WT_ON_MAIN: 0 (x-GEMM stream) 1.2234 ms, 1 1.2278, 2 1.2305 (A/B, 3 rounds); before it 1 was 0.4 % faster than 0
+#define CGR_W0E_ON_MAIN 1  // r02 (split-bf16): 1 258.0k vs 0 256.6k rxn/s (A/B, 3 rounds, within noise); r01: 0 (x-GEMM stream) 1.2234 ms, 1 1.2278, 2 1.2305
 #endif
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
@@ -205,10 +205,13 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
 #else
     if (CGR_B3) {
       ProfScope _p("gemm_nt_x", side);
+      // over padded x the GEMM runs to K = Fp (zero columns against the image's zero rows),
+      // the unmasked form, when that adds no k step to the image
+      const int Kx = (xa == fv.xp && fv.xp && b3_nk(d.Fp) == b3_nk(F)) ? (int)d.Fp : F;
       hipError_t e = with_vec(vx, [&](auto VX) {
         LdPlain<decltype(VX)::value> al{xa, ldx};
         EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
-        return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), ep, N, 2 * H, F, side);
+        return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), ep, N, 2 * H, Kx, side);
       });
       HIP_RET(e);
     } else {
@@ -309,7 +312,10 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     {
       ProfScope _p("gemm_nt_layer_fwd", st);
       const int vw = vec_for(Wl, H, H);
-      hipError_t e = CGR_B3 ? launch_b3nt(al, static_cast<const b3_u4*>(fv.b3lf[l]), ep, E, H, H, st)
+      const bool planes = CGR_B3 && CGR_B3TP && (training & CGR_TRAIN_FOR_BACKWARD) && fv.mhi[l];
+      hipError_t e = planes ? launch_b3nt(al, static_cast<const b3_u4*>(fv.b3lf[l]), ep, E, H, H, st,
+                                          B3PlaneOut{fv.mhi[l], fv.mlo[l], fv.mld})
+                   : CGR_B3 ? launch_b3nt(al, static_cast<const b3_u4*>(fv.b3lf[l]), ep, E, H, H, st)
                    : use_rs(H, H, H, Wl) ? with_rs_fmax(H, [&](auto FM) {
         return launch_gemm_rs<CGR_RS_RM, decltype(FM)::value>(al, Wl, H, ep, E, H, H, st);
       }) : with_vec(vw, [&](auto VW) {

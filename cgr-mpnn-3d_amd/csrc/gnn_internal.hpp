@@ -92,6 +92,11 @@ struct FloatView {
   void* b3rob;                    // W_n[:, F:]^T               (readout backward)
   void* b3lf[CGR_MAX_DEPTH];      // W_l                        (layer forward)
   void* b3lb[CGR_MAX_DEPTH];      // W_l^T                      (layer backward)
+  // the layer messages m_l = a_l[src] - h_l[rev] as bf16 hi / lo planes [round_up(E, 32)][mld]
+  // (written by the layer forward when the backward will run; gemm_b3tp.hpp's B operand)
+  uint16_t* mhi[CGR_MAX_DEPTH];
+  uint16_t* mlo[CGR_MAX_DEPTH];
+  int64_t mld;
 };
 
 struct Dims {
@@ -111,6 +116,7 @@ struct ArenaLayout {
   size_t e_s, w0eT, P, Q, xp, wT, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1], pre[CGR_MAX_DEPTH + 1], zn, hn,
       g;
   size_t b3x, b3rof, b3rob, b3lf[CGR_MAX_DEPTH], b3lb[CGR_MAX_DEPTH];
+  size_t mhi[CGR_MAX_DEPTH], mlo[CGR_MAX_DEPTH];
 };
 
 // 1: every side-stream weight gradient gets its own split-K slab and all of them are reduced in
@@ -121,6 +127,12 @@ struct ArenaLayout {
 #endif
 #ifndef CGR_BATCH_REDUCE_BLOCKS
 #define CGR_BATCH_REDUCE_BLOCKS 1024
+#endif
+#ifndef CGR_B3TP
+#define CGR_B3TP 0  // layer weight gradients from bf16 operand planes the producers write
+                    // (gemm_b3tp.hpp; lab 38 vs 50 us, but A/B -2.5 %: in the step the plane TN
+                    // runs no faster beside the main chain and the plane writes slow the layer
+                    // forward and the activation backward)
 #endif
 #ifndef CGR_DH0_DEFER
 #define CGR_DH0_DEFER 0  // 1: the skip gradient dh0 = sum_l sigma_l dpre_l is summed once by the
@@ -141,6 +153,7 @@ struct WorkspaceLayout {
   size_t bytes;
   size_t dpre[CGR_MAX_DEPTH], dm, dh0, dzn, ds, Gs, dg, slab, bslab, slab2, bslab2, dsig_part,
       slab_elems, bslab_elems;
+  size_t dphi[CGR_MAX_DEPTH], dplo[CGR_MAX_DEPTH];  // dpre bf16 planes (same ring as dpre)
   int dsig_blocks;
 };
 

@@ -427,6 +427,25 @@ hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_gra
 // ------------------------------------------------------------------------------------------
 int layer_act_bwd_blocks(int64_t E, int Hp) { return (int)cdiv(E * (Hp / 4), 256); }
 
+// 2 fp32 -> packed bf16x2 (RNE) and the values it represents (gemm_b3.hpp b3_cvt2)
+typedef __bf16 kb_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float kb_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t kb_cvt2(float a, float b, float& fa, float& fb) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(kb_f2{a, b}, kb_bf16x2));
+  fa = __uint_as_float(u << 16);
+  fb = __uint_as_float(u & 0xffff0000u);
+  return u;
+}
+// hi = bf16(x), lo = bf16(x - hi) of 4 values -> 8 bytes each at hi_p / lo_p
+__device__ __forceinline__ void kb_planes4(const float (&d)[4], uint16_t* hi_p, uint16_t* lo_p) {
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  float f0, f1, f2, f3, g0, g1, g2, g3;
+  const uint32_t h01 = kb_cvt2(d[0], d[1], f0, f1), h23 = kb_cvt2(d[2], d[3], f2, f3);
+  const uint32_t l01 = kb_cvt2(d[0] - f0, d[1] - f1, g0, g1), l23 = kb_cvt2(d[2] - f2, d[3] - f3, g2, g3);
+  *reinterpret_cast<u2*>(hi_p) = u2{h01, h23};
+  *reinterpret_cast<u2*>(lo_p) = u2{l01, l23};
+}
+
 // one float4 of one edge row of the layer backward, given dh = dL/dh_{l+1}[i, n..n+3]:
 // dpre = dh * keep/(1-p) * act'(pre) ; dh0 (+)= sigma * dpre ; dsig += dpre . h0
 __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
@@ -452,6 +471,10 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
   }
   const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
   *reinterpret_cast<float4*>(a.dpre + o) = dp;
+  if (a.dphi) {
+    const int64_t po = i * a.dpld + n;
+    kb_planes4(d, a.dphi + po, a.dplo + po);
+  }
   if (a.dh0) {
     const float sg = a.sigma ? a.sigma[0] : 1.f;
     float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);

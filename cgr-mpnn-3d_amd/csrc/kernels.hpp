@@ -75,6 +75,10 @@ struct LayerBwdArgs {
   int nl;
   const float* dpre_l[32];
   const float* sigma_l[32];
+  // dpre also as bf16 hi / lo planes [.][dpld] (the weight-gradient GEMM's A operand), or null
+  uint16_t* dphi;
+  uint16_t* dplo;
+  int64_t dpld;
 };
 // nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
 hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);

@@ -557,3 +557,31 @@ def test_mostly_unbonded_atoms_vs_oracle(act, skip, cuda_device):
     b = _sparse_batch(6, 40, seed=27)
     assert b.x.shape[0] > b.edge_index.shape[1]
     _oracle_compare(b, 64, 3, act, skip, cuda_device)
+
+
+# ---------------------------------------------------------------------------------------------
+# the two weight-gradient forms: operand planes written by the producers (forward flagged
+# CGR_TRAIN_FOR_BACKWARD, the module's training step) vs split staging inside the TN kernel
+# (forward without the flag); same arithmetic, different summation order
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("E_odd", [False, True])
+def test_weight_gradient_plane_and_staging_forms_agree(E_odd, cuda_device):
+    # E = 16 x 64 = 1024 (whole 32-row steps) or 37 x 58 = 2146 (zero-padded last step)
+    b = (make_batch(37, n_atoms=23, n_bonds=29, n_mace=32, seed=77) if E_odd
+         else make_batch(16, n_atoms=30, n_bonds=32, n_mace=32, seed=77))
+    data = b.to_torch(cuda_device)
+    F_, Fe, H, D = b.x.shape[1], 14, 400, 3
+    torch.manual_seed(5)
+    m = GNN(F_, Fe, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.1] * D).to(cuda_device)
+    params = [q.detach().contiguous() for q in m.native_parameters()]
+    runs = []
+    for prep in (True, False):
+        r = ArenaRun(_cfg_tuple(F_, Fe, H, D, "relu", False), data.x, data.edge_index,
+                     data.edge_attr, data.batch, data.ptr, b.num_graphs, params,
+                     dropout_ps=[0.1] * D, seed=99, training=True, prepare_backward=prep)
+        runs.append((r.y.clone(), r.backward(torch.linspace(-1, 1, b.num_graphs,
+                                                            device=cuda_device), params)))
+    assert torch.equal(runs[0][0], runs[1][0])
+    for ga, gb in zip(runs[0][1], runs[1][1]):
+        scale = gb.abs().max().item() + 1e-30
+        assert (ga - gb).abs().max().item() <= 2e-5 * scale
