@@ -156,6 +156,42 @@ struct EpLayer {
     }
     *reinterpret_cast<float4*>(hout + o) = make_float4(h[0], h[1], h[2], h[3]);
   }
+  // apply4p that also returns the stored values (rows / columns outside: v unchanged)
+  __device__ __forceinline__ float4 apply4p_h(int r, int c, float4 v, const Pre& p,
+                                              const Ctx& cx) const {
+    if (r >= M || c >= N) return v;
+    const int64_t o = (int64_t)r * ld + c;
+    float z[4] = {v.x, v.y, v.z, v.w};
+    const float h0v[4] = {p.h0.x, p.h0.y, p.h0.z, p.h0.w};
+    const float bv[4] = {p.b.x, p.b.y, p.b.z, p.b.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] = (z[k] + bv[k]) + cx.sg * h0v[k];
+    if (pre) *reinterpret_cast<float4*>(pre + o) = make_float4(z[0], z[1], z[2], z[3]);
+    float h[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      h[k] = act_fwd(z[k], act);
+      if (thresh)
+        h[k] = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
+                                                                                    : 0.f;
+      else
+        h[k] *= scale;
+    }
+    const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<float4*>(hout + o) = hv;
+    return hv;
+  }
+};
+
+// EpLayer whose GEMM also produces the layer's scatter-add a[v] = sum_{dst(e) = v} h'[e]
+// (GNN.py:134) for the dst segments lying wholly inside its row tile (rows are dst-sorted):
+// the tile's h' goes back through LDS and each segment is summed in row order, the order of
+// k_segsum_v4 (bitwise the unfused result).  Segments crossing a tile boundary and empty ones
+// are left to segsum_fixup (kernels.hip).
+struct EpLayerSeg : EpLayer {
+  const int* dst_s;  // [M] node of each (dst-sorted) row
+  float* aout;       // [nodes, lda]
+  int64_t lda;
 };
 
 // merged x-GEMM output [N, 2H]: columns [0, H) -> P (edge-init half), [H, 2H) -> Q (readout's

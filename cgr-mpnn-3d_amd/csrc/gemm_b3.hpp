@@ -31,6 +31,7 @@
 
 #include <type_traits>
 
+#include "epilogues.hpp"
 #include "gemm.hpp"
 
 namespace cgr {
@@ -174,7 +175,7 @@ struct B3NtShape {
   static constexpr int BPT = (BU4 + NT - 1) / NT;
   static constexpr int LDC = BN + 4;
   static constexpr size_t STAGE_BYTES = 3 * BU4 * 16;
-  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4;
+  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4;  // + EpLayerSeg's dst
   static constexpr size_t LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
 };
 
@@ -455,6 +456,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     pv[it] = ep.pre4(m0 + r, n0 + 4 * c4);
   }
   float* C = reinterpret_cast<float*>(b3_lds);
+  constexpr bool SEG = std::is_same<EP, EpLayerSeg>::value;
+  int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG: dst of rows m0 - 1 .. m0 + BM
+  if constexpr (SEG) {
+    for (int q = tid; q < BM + 2; q += NT) {
+      const int r = m0 - 1 + q;
+      sd[q] = (r >= 0 && r < M) ? ep.dst_s[r] : -1 - (r >= M);  // distinct sentinels
+    }
+  }
 #pragma unroll
   for (int i = 0; i < RF; ++i)
 #pragma unroll
@@ -469,7 +478,37 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     if (q < BM * C4) {
       const int r = q / C4, c4 = q - r * C4;
       const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
-      ep.apply4p(m0 + r, n0 + 4 * c4, v, pv[it], cx);
+      if constexpr (SEG)
+        *reinterpret_cast<float4*>(&C[r * S::LDC + 4 * c4]) =
+            ep.apply4p_h(m0 + r, n0 + 4 * c4, v, pv[it], cx);
+      else
+        ep.apply4p(m0 + r, n0 + 4 * c4, v, pv[it], cx);
+    }
+  }
+  if constexpr (SEG) {
+    // segments wholly inside [m0, m0 + nrow): thread (chunk of 16 rows, float4 column) sums the
+    // segments that START in its chunk, running past the chunk's end as needed
+    __syncthreads();
+    const int nrow = min(BM, M - m0);
+    constexpr int NCH = BM / 16;
+    for (int q = tid; q < NCH * C4; q += NT) {
+      const int ch = q / C4, c4 = q - ch * C4;
+      const int col = n0 + 4 * c4;
+      if (col >= ep.N) continue;
+      int s = 16 * ch;
+      const int end = min(16 * ch + 16, nrow);
+      // skip the tail of a segment begun before this chunk (in this tile or the previous one)
+      while (s < end && sd[s + 1] == sd[s]) ++s;
+      while (s < end) {
+        const int v = sd[s + 1];
+        float4 a = f4zero();
+        int r = s;
+        for (; r < nrow && sd[r + 1] == v; ++r)
+          a = f4add(a, *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]));
+        if (r < nrow || sd[nrow + 1] != v)  // ended inside the tile (else: crosses, fixup)
+          *reinterpret_cast<float4*>(ep.aout + (int64_t)v * ep.lda + col) = a;
+        s = r;
+      }
     }
   }
   B3_STAMP(3)
@@ -502,6 +541,9 @@ inline int b3nt_waves(int M, int N) {
   const int tiles_n = b3_cols(N).tiles;
   return ((M + 127) / 128) * tiles_n >= 192 ? 8 : 4;
 }
+
+// rows per workgroup tile of launch_b3nt for an M x N GEMM
+inline int b3nt_rows(int M, int N) { return b3nt_waves(M, N) == 8 ? 128 : 64; }
 
 // C = A B^T with B given as its image (b3_pack of the same N, K).  M, N, K > 0.
 template <class AL, class EP, class PO = B3NoPlanes>

@@ -18,6 +18,11 @@
 #include "profiling.hpp"
 #include "streams.hpp"
 
+#ifndef CGR_FUSED_SEGSUM
+#define CGR_FUSED_SEGSUM 0  // layer scatter-add in the layer GEMM's epilogue + a boundary fixup
+                            // (bitwise the unfused sums; the forward 5 us slower in the step:
+                            // the epilogue's segment pass costs more than the launch it saves)
+#endif
 #ifndef CGR_B3_PACK_MAIN
 #define CGR_B3_PACK_MAIN 1  // layer / readout weight images packed on the caller's stream
 #endif
@@ -295,6 +300,8 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     HIP_RET(segment_sum(fv.h[0], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[0], Hp, st));
   }
 
+  // the layer GEMM also sums the dst segments inside its row tiles (EpLayerSeg)
+  const bool fused_seg = CGR_B3 && CGR_FUSED_SEGSUM && Hp % 4 == 0;
   for (int l = 0; l < D; ++l) {
     const float* Wl = params[CGR_PARAM_CONV_W(l)];
     const float* bl_ = params[CGR_PARAM_CONV_B(l)];
@@ -313,9 +320,15 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       ProfScope _p("gemm_nt_layer_fwd", st);
       const int vw = vec_for(Wl, H, H);
       const bool planes = CGR_B3 && CGR_B3TP && (training & CGR_TRAIN_FOR_BACKWARD) && fv.mhi[l];
-      hipError_t e = planes ? launch_b3nt(al, static_cast<const b3_u4*>(fv.b3lf[l]), ep, E, H, H, st,
+      const b3_u4* img = static_cast<const b3_u4*>(fv.b3lf[l]);
+      const EpLayerSeg eps{ep, iv.dst_s, fv.a[l + 1], Hp};
+      hipError_t e = (fused_seg && planes)
+                         ? launch_b3nt(al, img, eps, E, H, H, st,
+                                       B3PlaneOut{fv.mhi[l], fv.mlo[l], fv.mld})
+                   : fused_seg ? launch_b3nt(al, img, eps, E, H, H, st)
+                   : planes ? launch_b3nt(al, img, ep, E, H, H, st,
                                           B3PlaneOut{fv.mhi[l], fv.mlo[l], fv.mld})
-                   : CGR_B3 ? launch_b3nt(al, static_cast<const b3_u4*>(fv.b3lf[l]), ep, E, H, H, st)
+                   : CGR_B3 ? launch_b3nt(al, img, ep, E, H, H, st)
                    : use_rs(H, H, H, Wl) ? with_rs_fmax(H, [&](auto FM) {
         return launch_gemm_rs<CGR_RS_RM, decltype(FM)::value>(al, Wl, H, ep, E, H, H, st);
       }) : with_vec(vw, [&](auto VW) {
@@ -328,7 +341,11 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       HIP_RET(e);
     }
     ProfScope _p2("segsum_dst_fwd", st);
-    HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
+    if (fused_seg)  // the GEMM summed the segments inside its row tiles
+      HIP_RET(segsum_fixup(fv.h[l + 1], Hp, iv.dst_ptr, N, Hp, b3nt_rows(E, H), fv.a[l + 1], Hp,
+                           st));
+    else
+      HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
   }
 
   // join: Q (split x-GEMM) and the backward transposes / images; the side stream is idle after this

@@ -45,6 +45,34 @@ __global__ __launch_bounds__(256) void k_segsum_v4(const float* __restrict__ val
   *reinterpret_cast<float4*>(out + v * ldo + 4 * c) = acc;
 }
 
+// segsum_fixup: thread (segment, float4 column); same row order as k_segsum_v4
+__global__ __launch_bounds__(256) void k_segsum_fixup(const float* __restrict__ vals, int64_t ldv,
+                                                      const int* __restrict__ ptr, int64_t nseg,
+                                                      int C4, int tile_rows,
+                                                      float* __restrict__ out, int64_t ldo) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nseg * C4) return;
+  const int64_t v = t / C4;
+  const int c = (int)(t - v * C4);
+  const int b = ptr[v], e = ptr[v + 1];
+  if (b < e && b / tile_rows == (e - 1) / tile_rows) return;  // written by its tile
+  float4 acc = f4zero();
+  for (int j = b; j < e; ++j)
+    acc = f4add(acc, *reinterpret_cast<const float4*>(vals + (int64_t)j * ldv + 4 * c));
+  *reinterpret_cast<float4*>(out + v * ldo + 4 * c) = acc;
+}
+
+hipError_t segsum_fixup(const float* vals, int64_t ldv, const int* ptr, int64_t nseg,
+                        int64_t width, int tile_rows, float* out, int64_t ldo, hipStream_t st) {
+  if (nseg <= 0 || width <= 0) return hipSuccess;
+  if (width % 4 || ldv % 4 || ldo % 4 || tile_rows <= 0) return hipErrorInvalidValue;
+  const int C4 = (int)(width / 4);
+  const int64_t tot = nseg * C4;
+  hipLaunchKernelGGL(k_segsum_fixup, dim3(cdiv(tot, 256)), dim3(256), 0, st, vals, ldv, ptr, nseg,
+                     C4, tile_rows, out, ldo);
+  return hipGetLastError();
+}
+
 template <bool GATHER>
 __global__ __launch_bounds__(256) void k_segsum_s(const float* __restrict__ vals, int64_t ldv,
                                                   const int* __restrict__ idx,

@@ -9,6 +9,10 @@ namespace cgr {
 // out[s, :w] = sum_{j in [ptr[s], ptr[s+1])} vals[idx ? idx[j] : j, :w]
 hipError_t segment_sum(const float* vals, int64_t ldv, const int* idx, const int* ptr,
                        int64_t nseg, int64_t width, float* out, int64_t ldo, hipStream_t st);
+// the segments segment_sum would write that a row-tiled producer (EpLayerSeg, tiles of
+// tile_rows rows from row 0) left out: empty ones and those crossing a tile boundary
+hipError_t segsum_fixup(const float* vals, int64_t ldv, const int* ptr, int64_t nseg,
+                        int64_t width, int tile_rows, float* out, int64_t ldo, hipStream_t st);
 
 struct TransposeJob {
   const float* src;  // [rows, ld_src], columns [col_off, col_off + cols)
