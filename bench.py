@@ -41,7 +41,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="cfg2", choices=["cfg1", "cfg2", "cfg4", "cfg5"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a HIP graph (1/0; -1 = auto: on for N = 1)")

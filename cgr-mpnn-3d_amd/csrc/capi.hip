@@ -224,9 +224,10 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     slab = s2 > slab ? s2 : slab;
     bslab = bs2 > bslab ? bs2 : bslab;
   }
-  auto b3acc = [&](int Nout, int Kout, int64_t R, int copies) {  // split-bf16 TN plans
+  auto b3acc = [&](int Nout, int Kout, int64_t R, int copies,
+                   int target = CGR_B3TN_TARGET) {  // split-bf16 TN plans
     if (!CGR_B3TN) return;
-    const TnPlan q = b3tn_tnplan(Nout, Kout, (int)R);
+    const TnPlan q = b3tn_tnplan(Nout, Kout, (int)R, target);
     const size_t s = (size_t)q.splits * Nout * (size_t)((Kout + 3) & ~3);
     const size_t bs = (size_t)q.splits * Nout;
     if (CGR_BATCH_REDUCE) {
@@ -237,7 +238,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
       bslab = bs > bslab ? bs : bslab;
     }
   };
-  b3acc(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N, 1);
+  b3acc(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N, 1, CGR_B3TN_RO_TARGET);
   b3acc(d.H, d.H, d.E, d.D);
   if (CGR_B3 && CGR_B3TP) {  // plane TN plans of the layer weight gradients
     const B3TpPlan q = b3tp_plan(d.H, d.H, (int)d.E);
@@ -281,7 +282,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
     slab = s2 > slab ? s2 : slab;
     bslab = bs2 > bslab ? bs2 : bslab;
     if (CGR_B3TN) {
-      const TnPlan b3 = b3tn_tnplan(d.H, Fx, (int)d.N);
+      const TnPlan b3 = b3tn_tnplan(d.H, Fx, (int)d.N, CGR_B3TN_NODE_TARGET);
       const size_t s3 = (size_t)b3.splits * d.H * (size_t)((Fx + 3) & ~3), bs3 = (size_t)b3.splits * d.H;
       slab = s3 > slab ? s3 : slab;
       bslab = bs3 > bslab ? bs3 : bslab;

@@ -59,8 +59,8 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
 template <class AL, class BL>
 static hipError_t b3tn_gemm(const char* name, const AL& al, const BL& bl, int Nout, int Kout, int R,
                             float* slab, float* bslab, bool want_bias, TnPlan* plan,
-                            hipStream_t st) {
-  const B3TnPlan q = b3tn_plan(Nout, Kout, R);
+                            hipStream_t st, int target = CGR_B3TN_TARGET) {
+  const B3TnPlan q = b3tn_plan(Nout, Kout, R, target);
   *plan = TnPlan{1, q.tiles_k, q.splits, q.rows_per_split};
   ProfScope _p(name, st);
   return launch_b3tn(al, bl, q, slab, bslab, Nout, Kout, R, want_bias, st);
@@ -189,7 +189,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dzn, Hp};
       LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
       if (CGR_B3TN && b3tn_ok(al, bl, H, N) && ((uintptr_t)fv.xp & 15) == 0) {
-        HIP_RET(b3tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side));
+        HIP_RET(b3tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, rsl, rbs, true, &p, side,
+                          CGR_B3TN_RO_TARGET));
       } else if (CGR_TNR_RO && tnr_x_ok(H, Fp + H, Fp, fv.xp)) {
         HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
                                 TnrConcat{fv.xp, Fp, fv.a[D], Hp, Fp}, H, Fp + H, N, rsl, rbs,
@@ -207,7 +208,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       const LdPlain<4> al4{dzn, Hp};
       const LdConcat<4> bl4{b->x, F, fv.a[D], Hp, F};
       if (CGR_B3TN && F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 && b3tn_ok(al4, bl4, H, N)) {
-        HIP_RET(b3tn_gemm("gemm_tn_wgrad_readout", al4, bl4, H, F + H, N, rsl, rbs, true, &p, side));
+        HIP_RET(b3tn_gemm("gemm_tn_wgrad_readout", al4, bl4, H, F + H, N, rsl, rbs, true, &p, side,
+                          CGR_B3TN_RO_TARGET));
       } else if (CGR_TNR_RO && F % 4 == 0 && tnr_x_ok(H, F + H, F, b->x)) {
         HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
                                 TnrConcat{b->x, F, fv.a[D], Hp, F}, H, F + H, N, rsl, rbs, true,
@@ -456,7 +458,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     const int Fx = fv.xp ? d.Fp : F;  // x columns the GEMM covers (pad columns are zero)
     const LdPlain<4> gal{Gs, Hp}, gbl{xb, ldx};
     if (CGR_B3TN && ldx % 4 == 0 && ((uintptr_t)xb & 15) == 0 && b3tn_ok(gal, gbl, H, N)) {
-      HIP_RET(b3tn_gemm("gemm_tn_wgrad_node", gal, gbl, H, Fx, N, slab2, bslab2, Fe == 0, &p, st));
+      HIP_RET(b3tn_gemm("gemm_tn_wgrad_node", gal, gbl, H, Fx, N, slab2, bslab2, Fe == 0, &p, st,
+                        CGR_B3TN_NODE_TARGET));
       HIP_RET(tn_reduce(p, slab2, bslab2, H, Fx, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st, F,
                         Fx - F, nullptr, CGR_NODE_REDUCE_FLAT));
     } else if (CGR_TNR_NODE && tnr_x_ok(H, Fx, ldx, xb)) {
