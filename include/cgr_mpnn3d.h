@@ -115,7 +115,12 @@ int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* batch, void* aren
  * dropout_p[l] > 0, from a counter-based RNG keyed by `seed` and, when `rng_counter` (device
  * uint64, may be NULL) is given, by its value, which the forward then increments on the device:
  * a captured graph replays with a fresh mask each time (the key is kept in the arena for the
- * backward).  Fills `arena` with what cgr_gnn_backward needs.  `y` device [B]. */
+ * backward).  Fills `arena` with what cgr_gnn_backward needs.  `y` device [B].
+ * `training` is a bit set: CGR_TRAIN_DROPOUT = train-mode dropout (module.training);
+ * CGR_TRAIN_FOR_BACKWARD = a backward will follow (the forward may then write operand forms only
+ * the weight-gradient GEMMs read).  Pass the same value to cgr_gnn_backward. */
+#define CGR_TRAIN_DROPOUT 1
+#define CGR_TRAIN_FOR_BACKWARD 2
 int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params,
                     const cgr_batch* batch, const float* dropout_p, uint64_t seed,
                     uint64_t* rng_counter, int32_t training, void* arena, float* y,
