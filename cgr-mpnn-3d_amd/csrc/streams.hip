@@ -24,8 +24,8 @@ bool single_stream() {
 
 // Keyed by the device of the caller's stream (the null stream: the current device).  The side
 // stream and its events are created on that device, whatever device is current.  The event ring
-// is per device and not locked: one host thread enqueues a device's forward / backward at a time
-// (the Python layer's use; two threads driving one device concurrently need their own process).
+// is per device; its users hold SideStreams::mu across each forward / backward enqueue, so
+// concurrent host threads on one device serialise their enqueues instead of sharing ring events.
 SideStreams* side_streams(hipStream_t main) {
   int dev = 0;
   if (main) {

@@ -7,12 +7,17 @@
 
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 namespace cgr {
 
 struct SideStreams {
   hipStream_t side;
   hipEvent_t ev[16];
   int next;
+  // held by cgr_gnn_forward / _backward for their whole enqueue: two host threads driving one
+  // device would otherwise re-record each other's ring events between a record and its wait
+  std::mutex mu;
 };
 
 // CGR_SINGLE_STREAM=1 in the environment: everything on the caller's stream (A/B of the
