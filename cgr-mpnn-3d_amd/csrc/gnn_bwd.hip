@@ -141,6 +141,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
 
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
+  std::lock_guard<std::mutex> ss_lock(ss->mu);
   // side-stream slabs: consecutive regions when batched (workspace_layout sizes them in the same
   // order: readout, layers D-1 .. 0, edge), else all at the start of the shared region
   RedJobs side_jobs{};
@@ -384,7 +385,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       // ring: dpre buffer (l-1) & 1 was last read by the weight gradient of layer l+1
       if (CGR_DPRE_RING && l + 1 <= D - 1) HIP_RET(hipStreamWaitEvent(st, tn_done[l + 1], 0));
       HIP_RET(segsum_act_bwd(layer_args(l - 1), iv.src_list, iv.src_ptr, iv.dst_ptr, N, false,
-                             st));
+                             iv.status, st));
     } else {
       LayerBwdArgs le{};
       le.dm = dm;
@@ -404,7 +405,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         }
       }
       le.dpre = dpre0;
-      HIP_RET(segsum_act_bwd(le, iv.src_list, iv.src_ptr, iv.dst_ptr, N, true, st));
+      HIP_RET(segsum_act_bwd(le, iv.src_list, iv.src_ptr, iv.dst_ptr, N, true, iv.status, st));
     }
   }
   float* gW0 = grads[CGR_PARAM_EDGE_INIT_W];

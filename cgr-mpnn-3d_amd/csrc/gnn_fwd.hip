@@ -92,6 +92,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
 #endif
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
+  std::lock_guard<std::mutex> ss_lock(ss->mu);
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
   hipStream_t side = (prof_enabled() || single_stream()) ? st : ss->side;
   HIP_RET(fork_to(ss, st, side));

@@ -13,7 +13,10 @@
 //   dst_ptr[N+1] CSR offsets of sorted positions per destination node
 //   src_ptr[N+1], src_list[E]  CSR of sorted positions per source node (stable by position)
 //   graph_ptr[B+1], node_graph[N]  node ranges per reaction graph
-//   status       bit0: edge index out of range, bit1: batch not sorted/out of range
+//   status       bit0: edge index out of range, bit1: batch not sorted/out of range,
+//                bit2: edges not reverse-paired (src(e ^ 1) != dst(e) for some e; informational:
+//                the reference's flip pairs e with e ^ 1 whatever they hold, and so does rev_s,
+//                but the backward's fused src sum takes its paired fast form only when clear)
 //
 // Determinism: the counting sort claims slots with atomics (arbitrary order inside a bucket) and
 // then insertion-sorts every bucket by key, so the result is the unique stable order.  Buckets are
@@ -171,11 +174,13 @@ __global__ void k_rev_place(const int* __restrict__ perm, const int* __restrict_
                             int* __restrict__ rev_s, const float* __restrict__ ea, int Fe,
                             int Fep, float* __restrict__ e_s, const int* __restrict__ src_s,
                             const int* __restrict__ src_ptr, int* __restrict__ cursor2,
-                            int* __restrict__ src_list) {
+                            int* __restrict__ src_list, const int* __restrict__ src_c,
+                            const int* __restrict__ dst_s, int* __restrict__ status) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= E) return;
   const int p = perm[i];
   rev_s[i] = inv[p ^ 1];
+  if (src_c[p ^ 1] != dst_s[i]) atomicOr(status, 4);
   if (Fep) {
     const float* src = ea + (int64_t)p * Fe;
     float* dst = e_s + (int64_t)i * Fep;
@@ -215,7 +220,7 @@ int cgr_graph_prep_impl(const PrepArgs& a, hipStream_t st) {
     // reverse map, sorted edge features, src CSR over sorted positions (stable by position)
     hipLaunchKernelGGL(k_rev_place, dim3(cdiv(E, T)), dim3(T), 0, st, iv.perm, iv.inv, E,
                        iv.rev_s, a.edge_attr, (int)a.Fe, (int)a.Fep, a.e_s, iv.src_s,
-                       iv.src_ptr, iv.cursor2, iv.src_list);
+                       iv.src_ptr, iv.cursor2, iv.src_list, iv.src_c, iv.dst_s, iv.status);
     hipLaunchKernelGGL(k_bucket_sort, dim3(cdiv(N, T)), dim3(T), 0, st, iv.src_ptr, N,
                        iv.src_list);
   }

@@ -587,53 +587,190 @@ hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Operands of one float4 of one edge row of the layer / edge-init backward, loaded ahead of the
+// row's dh (so a node's rows issue all their loads together); *_apply is bitwise layer_bwd_row /
+// edge_init_bwd_row given the same values.
+struct RowOps {
+  float4 m;    // h_{l+1} (ReLU mask) or pre (other activations); edge init: h_0 or pre_0
+  float4 acc;  // dh0 before this layer's accumulation (layer) / dh0 (edge init)
+  float4 h0;   // h_0 (learnable-skip partials)
+};
+
+__device__ __forceinline__ RowOps layer_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
+  const int64_t o = i * a.Hp + n;
+  RowOps r;
+  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.hnext : a.pre) + o);
+  r.acc = (a.dh0 && !a.first) ? *reinterpret_cast<const float4*>(a.dh0 + o) : f4zero();
+  r.h0 = a.dsig_part ? *reinterpret_cast<const float4*>(a.h0 + o) : f4zero();
+  return r;
+}
+
+__device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
+                                                uint64_t key, float& dsig, const RowOps& r) {
+  const int64_t o = i * a.Hp + n;
+  float d[4] = {dh.x, dh.y, dh.z, dh.w};
+  if (a.act == ACT_RELU) {
+    const float hh[4] = {r.m.x, r.m.y, r.m.z, r.m.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
+  } else {
+    const float zz[4] = {r.m.x, r.m.y, r.m.z, r.m.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float m = a.scale;
+      if (a.thresh && n + k < a.H)
+        m = drop_keep(key, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
+                                                                                      : 0.f;
+      d[k] = d[k] * m * act_grad(zz[k], a.act);
+    }
+  }
+  const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
+  *reinterpret_cast<float4*>(a.dpre + o) = dp;
+  if (a.dphi) {
+    const int64_t po = i * a.dpld + n;
+    kb_planes4(d, a.dphi + po, a.dplo + po);
+  }
+  if (a.dh0) {
+    const float sg = a.sigma ? a.sigma[0] : 1.f;
+    float4 acc = r.acc;
+    acc.x += sg * dp.x;
+    acc.y += sg * dp.y;
+    acc.z += sg * dp.z;
+    acc.w += sg * dp.w;
+    *reinterpret_cast<float4*>(a.dh0 + o) = acc;
+  }
+  if (a.dsig_part) {
+    const float hz[4] = {r.h0.x, r.h0.y, r.h0.z, r.h0.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (n + k < a.H) dsig += d[k] * hz[k];
+  }
+}
+
+__device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
+  const int64_t o = i * a.Hp + n;
+  RowOps r;
+  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.h0 : a.pre) + o);
+  r.acc = a.dh0 ? *reinterpret_cast<const float4*>(a.dh0 + o) : f4zero();
+  r.h0 = f4zero();
+  return r;
+}
+
+__device__ __forceinline__ void edge_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
+                                               const RowOps& r) {
+  const int64_t o = i * a.Hp + n;
+  float4 s0 = r.acc;
+  if (!a.dh0) {  // deferred skip gradient: the layers' dpre, in the layer loop's order
+    for (int l = a.nl - 1; l >= 0; --l) {
+      const float4 dp = *reinterpret_cast<const float4*>(a.dpre_l[l] + o);
+      const float sg = a.sigma_l[l] ? a.sigma_l[l][0] : 1.f;
+      s0.x += sg * dp.x;
+      s0.y += sg * dp.y;
+      s0.z += sg * dp.z;
+      s0.w += sg * dp.w;
+    }
+  }
+  float4 d = f4add(s0, dh);
+  if (a.act == ACT_RELU) {
+    d.x = r.m.x > 0.f ? d.x : 0.f;
+    d.y = r.m.y > 0.f ? d.y : 0.f;
+    d.z = r.m.z > 0.f ? d.z : 0.f;
+    d.w = r.m.w > 0.f ? d.w : 0.f;
+  } else {
+    d.x *= act_grad(r.m.x, a.act);
+    d.y *= act_grad(r.m.y, a.act);
+    d.z *= act_grad(r.m.z, a.act);
+    d.w *= act_grad(r.m.w, a.act);
+  }
+  *reinterpret_cast<float4*>(a.dpre + o) = d;
+}
+
 // src segmented sum of dm fused with the consumer of its result (the next lower layer's
 // activation backward, or the edge-init backward).  Thread (v, float4 column c):
-//   da[v] = sum_{src(e) = v} dm[e]       (rows gathered through src_list, the same row order and
-//                                         float4 adds as k_segsum_v4<true>: bitwise the unfused da)
+//   da[v] = sum_{src(e) = v} dm[e]
 //   for every edge i with dst(i) = v (contiguous in dst order):  dh = da[v] - dm[rev(i)], then
-//   layer_bwd_row / edge_init_bwd_row of row i.
-// da never reaches memory (the unfused pair wrote it and read it back gathered per edge).  The
-// grid is a.nblocks blocks (>= the threads needed) so the learnable-skip partial sums fill
+//   the layer / edge-init backward of row i.
+// Paired edges (graph prep's status bit 2 clear: src(e ^ 1) == dst(e) for every e, the CGR edge
+// order of graph_features.py:184-195) make {rev(i) : dst(i) = v} exactly {e : src(e) = v}: the
+// rows summed into da ARE the rows each incoming edge subtracts, so every dm row is loaded once
+// (in the order of v's incoming edges, four at a time with clamped indices, no branches), kept in
+// registers for the node's first four edges, and the rows' operands are loaded beside them.
+// Unpaired edge lists (any other edge_index) take the src-CSR gather.  da never reaches memory.
+// The grid is a.nblocks blocks (>= the threads needed) so the learnable-skip partial sums fill
 // exactly the slots the unfused kernel fills.
 template <bool EDGE_INIT>
 __global__ __launch_bounds__(256) void k_segsum_act_bwd(LayerBwdArgs a, const int* __restrict__ src_list,
                                                         const int* __restrict__ src_ptr,
-                                                        const int* __restrict__ dst_ptr, int64_t N) {
+                                                        const int* __restrict__ dst_ptr, int64_t N,
+                                                        const int* __restrict__ status) {
   const int C4 = a.Hp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float dsig = 0.f;
+  const bool paired = (*status & 4) == 0;
   if (t < N * C4) {
     const int64_t v = t / C4;
     const int n = 4 * (int)(t - v * C4);
     const float* base = a.dm + n;
     auto ld4 = [&](int64_t r) { return *reinterpret_cast<const float4*>(base + r * a.Hp); };
-    const int b = src_ptr[v], e = src_ptr[v + 1];
-    float4 da = f4zero();
-    int j = b;
-    for (; j + 4 <= e; j += 4) {
-      const int64_t r0 = src_list[j], r1 = src_list[j + 1], r2 = src_list[j + 2],
-                    r3 = src_list[j + 3];
-      const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2), x3 = ld4(r3);
-      da = f4add(f4add(f4add(f4add(da, x0), x1), x2), x3);
-    }
-    const int rem = e - j;
-    if (rem > 0) {
-      const int64_t r0 = src_list[j], r1 = src_list[min(j + 1, e - 1)],
-                    r2 = src_list[min(j + 2, e - 1)];
-      const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2);
-      da = f4add(da, x0);
-      if (rem > 1) da = f4add(da, x1);
-      if (rem > 2) da = f4add(da, x2);
-    }
+    auto loads = [&](int64_t i) {
+      if constexpr (EDGE_INIT) return edge_row_loads(a, i, n);
+      else return layer_row_loads(a, i, n);
+    };
     const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
+    auto apply = [&](int64_t i, float4 dh, const RowOps& r) {
+      if constexpr (EDGE_INIT) edge_row_apply(a, i, n, dh, r);
+      else layer_row_apply(a, i, n, dh, key, dsig, r);
+    };
     const int ib = dst_ptr[v], ie = dst_ptr[v + 1];
-    for (int i = ib; i < ie; ++i) {
-      const float4 dh = f4sub(da, ld4(a.rev_s[i]));
-      if constexpr (EDGE_INIT)
-        edge_init_bwd_row(a, i, n, dh);
-      else
-        layer_bwd_row(a, i, n, dh, key, dsig);
+    if (paired) {
+      const int deg = ie - ib;
+      float4 da = f4zero();
+      float4 r[4];
+      RowOps ops[4];
+      if (deg > 0) {
+        int ri[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ri[k] = a.rev_s[min(ib + k, ie - 1)];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) r[k] = ld4(ri[k]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ops[k] = loads(min(ib + k, ie - 1));
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < deg) da = f4add(da, r[k]);
+        for (int c = 4; c < deg; c += 4) {  // high-degree nodes: the rest of the sum
+          float4 x[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) x[k] = ld4(a.rev_s[min(ib + c + k, ie - 1)]);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (c + k < deg) da = f4add(da, x[k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (k < deg) apply(ib + k, f4sub(da, r[k]), ops[k]);
+        for (int i = ib + 4; i < ie; ++i) apply(i, f4sub(da, ld4(a.rev_s[i])), loads(i));
+      }
+    } else {
+      const int b = src_ptr[v], e = src_ptr[v + 1];
+      float4 da = f4zero();
+      int j = b;
+      for (; j + 4 <= e; j += 4) {
+        const int64_t r0 = src_list[j], r1 = src_list[j + 1], r2 = src_list[j + 2],
+                      r3 = src_list[j + 3];
+        const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2), x3 = ld4(r3);
+        da = f4add(f4add(f4add(f4add(da, x0), x1), x2), x3);
+      }
+      const int rem = e - j;
+      if (rem > 0) {
+        const int64_t r0 = src_list[j], r1 = src_list[min(j + 1, e - 1)],
+                      r2 = src_list[min(j + 2, e - 1)];
+        const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2);
+        da = f4add(da, x0);
+        if (rem > 1) da = f4add(da, x1);
+        if (rem > 2) da = f4add(da, x2);
+      }
+      for (int i = ib; i < ie; ++i) apply(i, f4sub(da, ld4(a.rev_s[i])), loads(i));
     }
   }
   if (!EDGE_INIT && a.dsig_part) block_partial(dsig, a.dsig_part);
@@ -644,17 +781,18 @@ int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp) {
 }
 
 hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int* src_ptr,
-                          const int* dst_ptr, int64_t N, bool edge_init, hipStream_t st) {
+                          const int* dst_ptr, int64_t N, bool edge_init, const int* status,
+                          hipStream_t st) {
   if (N <= 0 || a.Hp % 4) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
   // as many blocks as the unfused layer kernel when learnable-skip partials are written
   const int nb = (!edge_init && a.dsig_part) ? segsum_act_bwd_blocks(a.E, N, a.Hp)
                                              : (int)cdiv(N * (a.Hp / 4), 256);
   if (edge_init)
     hipLaunchKernelGGL(k_segsum_act_bwd<true>, dim3(nb), dim3(256), 0, st, a, src_list, src_ptr,
-                       dst_ptr, N);
+                       dst_ptr, N, status);
   else
     hipLaunchKernelGGL(k_segsum_act_bwd<false>, dim3(nb), dim3(256), 0, st, a, src_list,
-                       src_ptr, dst_ptr, N);
+                       src_ptr, dst_ptr, N, status);
   return hipGetLastError();
 }
 

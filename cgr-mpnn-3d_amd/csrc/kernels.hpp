@@ -91,8 +91,10 @@ int layer_act_bwd_blocks(int64_t E, int Hp);
 // dst is the segment's node (dh = da[dst(i)] - dm[rev(i)]), or with the edge-init backward
 // (edge_init: a.dh0 -> a.dpre in place, a.h0 / a.pre = h_0 / pre_0).  With learnable-skip
 // partials it launches segsum_act_bwd_blocks(E, N, Hp) blocks (size dsig_part accordingly).
+// status: graph prep's status word (bit 2 clear: paired edges, the fast form; see kernels.hip)
 hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int* src_ptr,
-                          const int* dst_ptr, int64_t N, bool edge_init, hipStream_t st);
+                          const int* dst_ptr, int64_t N, bool edge_init, const int* status,
+                          hipStream_t st);
 int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp);
 
 // dpre0 = (dh0 + da[dst_s] - dm[rev_s]) * act'(pre0)   (ReLU: h0 > 0)

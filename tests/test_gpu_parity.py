@@ -552,6 +552,35 @@ def _sparse_batch(num_graphs, n_atoms, seed):
                     edge_attr=np.concatenate(eas), batch=np.concatenate(bt), ptr=ptr, y=y)
 
 
+def _pair_status(b, dev):
+    data = b.to_torch(dev)
+    run = ArenaRun(_cfg_tuple(b.x.shape[1], b.edge_attr.shape[1], 32, 1, "relu", False), data.x,
+                   data.edge_index, data.edge_attr, data.batch, data.ptr, b.num_graphs,
+                   [p.detach() for p in GNN(b.x.shape[1], b.edge_attr.shape[1], depth=1,
+                                            hidden_sizes=[32]).to(dev).native_parameters()])
+    torch.cuda.synchronize()
+    return int(run.ints("status", 1).item())
+
+
+@pytest.mark.parametrize("act,skip", [("relu", True), ("gelu", False)])
+def test_unpaired_edge_order_vs_oracle(act, skip, cuda_device):
+    # edges shuffled inside every graph: e ^ 1 is no longer the reverse of e, and the reference
+    # still pairs them positionally (flip of view(E/2, 2, H), GNN.py:136-138).  Graph prep flags
+    # it (status bit 2) and the backward's fused src sum takes its src-CSR form instead of the
+    # paired one; results must still match the oracle.
+    from dataclasses import replace
+
+    b = make_batch(8, n_atoms=30, n_bonds=30, n_mace=16, seed=28)
+    per = b.edge_index.shape[1] // b.num_graphs
+    rng = np.random.default_rng(5)
+    order = np.concatenate([g * per + rng.permutation(per) for g in range(b.num_graphs)])
+    u = replace(b, edge_index=np.ascontiguousarray(b.edge_index[:, order]),
+                edge_attr=np.ascontiguousarray(b.edge_attr[order]))
+    assert _pair_status(b, cuda_device) == 0
+    assert _pair_status(u, cuda_device) == 4
+    _oracle_compare(u, 64, 3, act, skip, cuda_device)
+
+
 @pytest.mark.parametrize("act,skip", [("relu", True), ("silu", True), ("relu", False)])
 def test_mostly_unbonded_atoms_vs_oracle(act, skip, cuda_device):
     b = _sparse_batch(6, 40, seed=27)
