@@ -216,15 +216,28 @@ __device__ unsigned long long* b3_stamps;  // lab: [block][wave][4] s_memrealtim
 // writes the k steps ks with ks % tiles_n == tn (each A element is loaded by every column tile).
 struct B3NoPlanes {
   static constexpr bool on = false;
+  static constexpr bool copy = false;
   uint16_t* hi;
   uint16_t* lo;
   int64_t ld;
 };
 struct B3PlaneOut {
   static constexpr bool on = true;
+  static constexpr bool copy = false;
   uint16_t* hi;
   uint16_t* lo;
   int64_t ld;  // >= nk * 32
+};
+// Other by-product: the A operand itself as fp32 rows of `cols` floats (ld, 16-byte aligned rows),
+// the masked values the split reads (zeros at k >= K): the x-GEMM reads x as it comes (8-byte rows)
+// and leaves the 16-byte-row copy the weight-gradient GEMMs read, instead of a padding pass ahead
+// of it.  Column tile tn writes the k steps ks with ks % tiles_n == tn.
+struct B3RowCopy {
+  static constexpr bool on = false;
+  static constexpr bool copy = true;
+  float* dst;
+  int64_t ld;
+  int cols;  // multiple of 4
 };
 
 template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP, class PO = B3NoPlanes>
@@ -271,6 +284,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       }
       const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
       b3_split8<3>(f, af[i]);
+      if constexpr (PO::copy) {
+        const int row = m0 + (w * RF + i) * 16 + fr;
+        if (ks % tiles_n == tn && row < M) {
+          float* o = po.dst + (int64_t)row * po.ld + kb;
+          if (kb < po.cols) *reinterpret_cast<float4*>(o) = u;
+          if (kb + 16 < po.cols) *reinterpret_cast<float4*>(o + 16) = v;
+        }
+      }
       if constexpr (PO::on) {
         const int row = m0 + (w * RF + i) * 16 + fr;
         if (ks % tiles_n == tn && row < ((M + 31) & ~31) && ks < nk) {

@@ -36,6 +36,10 @@
 #ifndef CGR_PAD_ON_MAIN
 #define CGR_PAD_ON_MAIN 0
 #endif
+#ifndef CGR_B3_XCOPY
+#define CGR_B3_XCOPY 0  // 1: x-GEMM on unpadded x (8-byte loads) writes the padded copy xp itself
+                        // (no padding pass); A/B 270.3k -> 251.7k rxn/s (-7 %), off
+#endif
 
 namespace cgr {
 
@@ -102,8 +106,11 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   // read xp with 16-byte loads
   const float* xa = b->x;
   int64_t ldx = F;
+  // CGR_B3_XCOPY: no padding pass; the x-GEMM reads x with 8-byte loads and writes xp itself
+  const bool xcopy = CGR_B3 && CGR_B3_XCOPY && !CGR_B3_SPLIT_X && !CGR_SPLIT_XGEMM && fv.xp &&
+                     vec_for(b->x, F, F) >= 2;
 #if !CGR_PAD_ON_MAIN
-  if (fv.xp) {
+  if (fv.xp && !xcopy) {
     ProfScope _p("pad_x", side);
     HIP_RET(pad_rows(b->x, N, F, fv.xp, d.Fp, side));
     xa = fv.xp;
@@ -217,6 +224,9 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       hipError_t e = with_vec(vx, [&](auto VX) {
         LdPlain<decltype(VX)::value> al{xa, ldx};
         EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
+        if (xcopy)
+          return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), ep, N, 2 * H, Kx, side,
+                             B3RowCopy{fv.xp, d.Fp, (int)d.Fp});
         return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), ep, N, 2 * H, Kx, side);
       });
       HIP_RET(e);
