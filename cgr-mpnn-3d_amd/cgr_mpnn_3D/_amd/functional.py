@@ -47,7 +47,8 @@ def _dropout_array(dropout_ps, depth):
 
 
 def read_status(arena, cfg, N, E, B) -> int:
-    """Graph-prep status word (bit0 bad edge index, bit1 bad/unsorted batch).  Synchronises."""
+    """Graph-prep status word (bit0 bad edge index, bit1 bad/unsorted batch, bit2 edges not
+    reverse-paired: informational).  Synchronises."""
     lib = native.load()
     off = lib.cgr_gnn_arena_offset(ctypes.byref(cfg), N, E, B, b"status", 0)
     return int(arena[off:off + 4].view(torch.int32).item())

@@ -105,6 +105,9 @@ ArenaLayout arena_layout(const Dims& d) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
     L.a[l] = l <= d.D ? b.take(4 * N * Hp) : kNone;
     L.pre[l] = (l <= d.D && d.act != CGR_ACT_RELU) ? b.take(4 * E * Hp) : kNone;
+    // h_0's mask comes from the fused edge init (Hp <= 512), every layer's from its epilogue
+    L.hb[l] = (CGR_HBITS && l <= d.D && d.act == CGR_ACT_RELU && (l > 0 || Hp <= 512))
+                  ? b.take(E * (Hp / 4)) : kNone;
   }
   L.zn = d.act != CGR_ACT_RELU ? b.take(4 * N * Hp) : kNone;
   L.hn = b.take(4 * N * Hp);
@@ -156,6 +159,7 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
     f.h[l] = (float*)at(arena, L.h[l]);
     f.a[l] = (float*)at(arena, L.a[l]);
     f.pre[l] = (float*)at(arena, L.pre[l]);
+    f.hb[l] = (uint8_t*)at(arena, L.hb[l]);
   }
   f.zn = (float*)at(arena, L.zn);
   f.hn = (float*)at(arena, L.hn);

@@ -79,6 +79,7 @@ struct EpLayer {
   float scale;      // 1 / (1 - p)
   const uint64_t* seed;  // device: the forward's dropout key (arena "rng"); read iff thresh
   int layer;
+  uint8_t* hbits = nullptr;  // [M, ld/4] masks h > 0 (4 bits per float4; apply4p paths only)
   __device__ __forceinline__ void operator()(int r, int c, float v) const {
     if (r >= M || c >= N) return;
     const int64_t o = (int64_t)r * ld + c;
@@ -155,6 +156,9 @@ struct EpLayer {
         h[k] *= scale;
     }
     *reinterpret_cast<float4*>(hout + o) = make_float4(h[0], h[1], h[2], h[3]);
+    if (hbits)
+      hbits[(int64_t)r * (ld >> 2) + (c >> 2)] =
+          (uint8_t)((h[0] > 0.f) | ((h[1] > 0.f) << 1) | ((h[2] > 0.f) << 2) | ((h[3] > 0.f) << 3));
   }
   // apply4p that also returns the stored values (rows / columns outside: v unchanged)
   __device__ __forceinline__ float4 apply4p_h(int r, int c, float4 v, const Pre& p,
@@ -179,6 +183,9 @@ struct EpLayer {
     }
     const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
     *reinterpret_cast<float4*>(hout + o) = hv;
+    if (hbits)
+      hbits[(int64_t)r * (ld >> 2) + (c >> 2)] =
+          (uint8_t)((h[0] > 0.f) | ((h[1] > 0.f) << 1) | ((h[2] > 0.f) << 2) | ((h[3] > 0.f) << 3));
     return hv;
   }
 };

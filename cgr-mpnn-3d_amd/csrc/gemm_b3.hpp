@@ -148,6 +148,15 @@ struct B3PackJobs {
   int n;
 };
 hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st);
+// x rows padded to ldp floats (F % 4 != 0), the same launch as the image jobs: the padding pass
+// and the x-GEMM's image pack run side by side instead of back to back
+struct B3PadJob {
+  const float* x;
+  int64_t N;
+  int F, ldp;
+  float* xp;
+};
+hipError_t b3_pack_pad(const B3PackJobs& jobs, const B3PadJob& pad, hipStream_t st);
 // append a job, launching the batch when it is full
 inline hipError_t b3_pack_add(B3PackJobs& jobs, const B3PackJob& j, hipStream_t st) {
   if (jobs.n == kMaxB3PackJobs) {

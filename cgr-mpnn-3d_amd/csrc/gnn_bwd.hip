@@ -171,10 +171,20 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // head + readout
   {
     ProfScope _p("head_readout_bwd", st);
-    HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
-                     grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], st));
-    HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H, Hp,
-                            d.act, dzn, st));
+#ifndef CGR_HEAD_MERGE
+#define CGR_HEAD_MERGE 0  // 1: dwf / dbf column sums as extra blocks of the dzn launch (one launch
+                          // less on the critical chain, 15 -> 9.5 us, but the step A/B -1.4 %)
+#endif
+    if (CGR_HEAD_MERGE) {
+      HIP_RET(head_readout_bwd(dy, fv.g, d.B, grads[CGR_PARAM_FFN_W(D)],
+                               grads[CGR_PARAM_FFN_B(D)], params[CGR_PARAM_FFN_W(D)],
+                               iv.node_graph, fv.hn, fv.zn, N, H, Hp, d.act, dzn, st));
+    } else {
+      HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
+                       grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], st));
+      HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
+                              Hp, d.act, dzn, st));
+    }
   }
   // side: dW_n = dzn^T [x | s], db_n.  Enqueued here (CGR_RO_TN_AT < 0) or after the layer
   // weight gradient of layer CGR_RO_TN_AT, so that it does not run beside the main stream's
@@ -276,6 +286,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.dst_s = iv.dst_s;
     la.rev_s = iv.rev_s;
     la.hnext = fv.h[l + 1];
+    la.hbits = fv.hb[l + 1];
     la.pre = fv.pre[l + 1];
     la.h0 = fv.h[0];
     la.sigma = d.learnable_skip ? params[CGR_PARAM_SKIP(D, l)] : nullptr;
@@ -391,6 +402,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       le.dm = dm;
       le.rev_s = iv.rev_s;
       le.h0 = fv.h[0];
+      le.hbits = fv.hb[0];
       le.pre = fv.pre[0];
       le.act = d.act;
       le.E = E;

@@ -72,6 +72,10 @@ struct IndexView {
 #endif
 
 // Forward-saved float state inside the arena.
+#ifndef CGR_HBITS
+#define CGR_HBITS 0  // 1: ReLU masks as bits for the backward (FloatView::hb); A/B -2.4 % (the
+                     // byte stores slow the layer epilogues 2-4 us, the backward did not gain)
+#endif
 struct FloatView {
   float* e_s;   // [E, Fep] sorted, zero padded edge_attr
   float* w0eT;  // [Fe, Hp] transposed edge-feature slice of edge_init.weight
@@ -97,6 +101,10 @@ struct FloatView {
   uint16_t* mhi[CGR_MAX_DEPTH];
   uint16_t* mlo[CGR_MAX_DEPTH];
   int64_t mld;
+  // ReLU only (CGR_HBITS): the backward's activation masks h_l > 0 as [E, Hp/4] bytes, bit k of
+  // byte (i, c) = h_l[i, 4c + k] > 0, written beside h_l by its producer (edge init / layer
+  // epilogue); the backward reads 1/32 of the bytes of h_l for them.  nullptr: read h_l.
+  uint8_t* hb[CGR_MAX_DEPTH + 1];
 };
 
 struct Dims {
@@ -117,6 +125,7 @@ struct ArenaLayout {
       g;
   size_t b3x, b3rof, b3rob, b3lf[CGR_MAX_DEPTH], b3lb[CGR_MAX_DEPTH];
   size_t mhi[CGR_MAX_DEPTH], mlo[CGR_MAX_DEPTH];
+  size_t hb[CGR_MAX_DEPTH + 1];
 };
 
 // 1: every side-stream weight gradient gets its own split-K slab and all of them are reduced in

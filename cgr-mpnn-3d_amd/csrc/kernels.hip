@@ -218,7 +218,7 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
     const float* __restrict__ P, const int* __restrict__ src_s, const float* __restrict__ e_s,
     int Fe, int Fep, const float* __restrict__ w0eT, const float* __restrict__ b0,
     const int* __restrict__ dst_ptr, int64_t N, int H, int Hp, int act, float* __restrict__ h0,
-    float* __restrict__ pre0, float* __restrict__ a) {
+    float* __restrict__ pre0, float* __restrict__ a, uint8_t* __restrict__ h0bits) {
   const int C4 = Hp >> 2;
   const int c = threadIdx.x;
   if (c >= C4) return;  // no barriers below
@@ -277,6 +277,9 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
       h.z = act_fwd(z.z, act);
       h.w = act_fwd(z.w, act);
       *reinterpret_cast<float4*>(h0 + o) = h;
+      if (h0bits)
+        h0bits[(int64_t)i * C4 + c] = (uint8_t)((h.x > 0.f) | ((h.y > 0.f) << 1) |
+                                                ((h.z > 0.f) << 2) | ((h.w > 0.f) << 3));
       acc = f4add(acc, h);
     }
     *reinterpret_cast<float4*>(a + v * Hp + n) = acc;
@@ -286,17 +289,17 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
 hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
                                 int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
                                 int64_t N, int H, int Hp, int act, float* h0, float* pre0,
-                                float* a, hipStream_t st) {
+                                float* a, hipStream_t st, uint8_t* h0bits) {
   if (N <= 0) return hipSuccess;
   if (Hp % 4 || Hp / 4 > 128) return hipErrorInvalidValue;  // one thread per float4 column
   const int threads = (Hp / 4 + 63) / 64 * 64;
   const int nb = (int)cdiv(N, kEiNodes);
   if (Fe <= kEiMaxFe && (Fe == 0 || Fep % 4 == 0))
     hipLaunchKernelGGL(k_edge_init_seg<true>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
-                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a, h0bits);
   else
     hipLaunchKernelGGL(k_edge_init_seg<false>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
-                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a, h0bits);
   return hipGetLastError();
 }
 
@@ -404,13 +407,63 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
   return hipGetLastError();
 }
 
+// Head blocks of k_readout_bwd (blocks past the dzn ones): 64 columns x 4 row phases each;
+// dwf[n] = sum_b dy[b] g[b, n], dbf = sum_b dy[b], phases combined in fixed order.
+struct HeadBwd {
+  const float* g;
+  int64_t B;
+  float* dwf;
+  float* dbf;
+  int first_block;  // blocks below compute dzn
+};
+
+__device__ __forceinline__ void head_bwd_block(const float* __restrict__ dy, const HeadBwd& hb,
+                                               int blk, int H, int Hp) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int n = blk * 64 + tx;
+  float acc = 0.f, sdy = 0.f;
+  const int B = (int)hb.B;
+  const int nc = n < H ? n : H - 1;
+  int b = ty;
+  for (; b + 28 < B; b += 32) {  // 8 rows' loads in flight per thread (latency, not bandwidth)
+    float d[8], gv[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      d[j] = dy[b + 4 * j];
+      gv[j] = hb.g[(int64_t)(b + 4 * j) * Hp + nc];
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      acc += d[j] * gv[j];
+      sdy += d[j];
+    }
+  }
+  for (; b < B; b += 4) {
+    const float d = dy[b];
+    acc += d * hb.g[(int64_t)b * Hp + nc];
+    sdy += d;
+  }
+  __shared__ float red[2][4][64];
+  red[0][ty][tx] = acc;
+  red[1][ty][tx] = sdy;  // every tx of a row phase summed the same dy values
+  __syncthreads();
+  if (ty == 0 && n < H)
+    hb.dwf[n] = (red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]);
+  if (blk == 0 && threadIdx.x == 0)
+    hb.dbf[0] = (red[1][0][0] + red[1][1][0]) + (red[1][2][0] + red[1][3][0]);
+}
+
 __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dy,
                                                      const float* __restrict__ wf,
                                                      const int* __restrict__ node_graph,
                                                      const float* __restrict__ hn,
                                                      const float* __restrict__ zn, int64_t N,
                                                      int H, int Hp, int act,
-                                                     float* __restrict__ dzn) {
+                                                     float* __restrict__ dzn, HeadBwd hb) {
+  if ((int)blockIdx.x >= hb.first_block) {
+    head_bwd_block(dy, hb, (int)blockIdx.x - hb.first_block, H, Hp);
+    return;
+  }
   const int C4 = Hp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * C4) return;
@@ -443,10 +496,21 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
                            float* dzn, hipStream_t st) {
-  if (N <= 0) return hipSuccess;
-  const int64_t tot = N * (Hp / 4);
-  hipLaunchKernelGGL(k_readout_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dy, wf, node_graph, hn,
-                     zn, N, H, Hp, act, dzn);
+  return head_readout_bwd(dy, nullptr, 0, nullptr, nullptr, wf, node_graph, hn, zn, N, H, Hp, act,
+                          dzn, st);
+}
+
+hipError_t head_readout_bwd(const float* dy, const float* g, int64_t B, float* dwf, float* dbf,
+                            const float* wf, const int* node_graph, const float* hn,
+                            const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
+                            hipStream_t st) {
+  const int64_t tot = N > 0 ? N * (Hp / 4) : 0;
+  const int rb = (int)cdiv(tot, 256);
+  const int hbk = dwf ? (int)cdiv(H, 64) : 0;
+  if (rb + hbk <= 0) return hipSuccess;
+  const HeadBwd hb{g, B, dwf, dbf, rb};
+  hipLaunchKernelGGL(k_readout_bwd, dim3(rb + hbk), dim3(256), 0, st, dy, wf, node_graph, hn, zn,
+                     N, H, Hp, act, dzn, hb);
   return hipGetLastError();
 }
 
@@ -474,6 +538,18 @@ __device__ __forceinline__ void kb_planes4(const float (&d)[4], uint16_t* hi_p, 
   *reinterpret_cast<u2*>(lo_p) = u2{l01, l23};
 }
 
+// ReLU mask of a float4 (bits of FloatView::hb when given, else the sign of h): as float4 of
+// 1 / 0 in m so the consumers test m.k > 0 either way
+__device__ __forceinline__ float4 relu_mask4(const uint8_t* bits, const float* h, int64_t i,
+                                             int n, int Hp) {
+  if (bits) {
+    const uint32_t b = bits[i * (Hp >> 2) + (n >> 2)];
+    return make_float4((float)(b & 1), (float)((b >> 1) & 1), (float)((b >> 2) & 1),
+                       (float)((b >> 3) & 1));
+  }
+  return *reinterpret_cast<const float4*>(h + i * Hp + n);
+}
+
 // one float4 of one edge row of the layer backward, given dh = dL/dh_{l+1}[i, n..n+3]:
 // dpre = dh * keep/(1-p) * act'(pre) ; dh0 (+)= sigma * dpre ; dsig += dpre . h0
 __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
@@ -481,7 +557,7 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
   const int64_t o = i * a.Hp + n;
   float d[4] = {dh.x, dh.y, dh.z, dh.w};
   if (a.act == ACT_RELU) {  // h_{l+1} > 0 <=> relu active and kept by dropout
-    const float4 hv = *reinterpret_cast<const float4*>(a.hnext + o);
+    const float4 hv = relu_mask4(a.hbits, a.hnext, i, n, a.Hp);
     const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
@@ -599,7 +675,8 @@ struct RowOps {
 __device__ __forceinline__ RowOps layer_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
   const int64_t o = i * a.Hp + n;
   RowOps r;
-  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.hnext : a.pre) + o);
+  r.m = a.act == ACT_RELU ? relu_mask4(a.hbits, a.hnext, i, n, a.Hp)
+                          : *reinterpret_cast<const float4*>(a.pre + o);
   r.acc = (a.dh0 && !a.first) ? *reinterpret_cast<const float4*>(a.dh0 + o) : f4zero();
   r.h0 = a.dsig_part ? *reinterpret_cast<const float4*>(a.h0 + o) : f4zero();
   return r;
@@ -650,7 +727,8 @@ __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i
 __device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
   const int64_t o = i * a.Hp + n;
   RowOps r;
-  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.h0 : a.pre) + o);
+  r.m = a.act == ACT_RELU ? relu_mask4(a.hbits, a.h0, i, n, a.Hp)
+                          : *reinterpret_cast<const float4*>(a.pre + o);
   r.acc = a.dh0 ? *reinterpret_cast<const float4*>(a.dh0 + o) : f4zero();
   r.h0 = f4zero();
   return r;

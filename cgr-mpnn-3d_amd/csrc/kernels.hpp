@@ -34,7 +34,7 @@ hipError_t transpose_batch(const TransposeJobs& jobs, hipStream_t st);
 hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
                                 int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
                                 int64_t N, int H, int Hp, int act, float* h0, float* pre0,
-                                float* a, hipStream_t st);
+                                float* a, hipStream_t st, uint8_t* h0bits = nullptr);
 hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int Fe, int Fep,
                          const float* w0eT, const float* b0, int64_t E, int H, int Hp, int act,
                          float* h0, float* pre0, hipStream_t st);
@@ -48,6 +48,12 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
                     float* dg, float* dwf, float* dbf, hipStream_t st);
 
 // dzn[v] = dy[graph(v)] * wf * act'(zn[v])   (ReLU: hn > 0)
+// k_head_bwd's dwf / dbf column sums and readout_act_bwd's dzn in one launch (head blocks after
+// the dzn blocks)
+hipError_t head_readout_bwd(const float* dy, const float* g, int64_t B, float* dwf, float* dbf,
+                            const float* wf, const int* node_graph, const float* hn,
+                            const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
+                            hipStream_t st);
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
                            float* dzn, hipStream_t st);
@@ -60,6 +66,7 @@ struct LayerBwdArgs {
   const int* dst_s;
   const int* rev_s;
   const float* hnext;  // h_{l+1} (ReLU mask)
+  const uint8_t* hbits;  // its mask bits (FloatView::hb; edge init: h_0's), or nullptr
   const float* pre;    // pre_{l} (non-ReLU)
   const float* h0;
   const float* sigma;  // skip weight (nullptr -> 1)

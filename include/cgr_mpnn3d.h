@@ -97,7 +97,10 @@ int64_t cgr_gnn_arena_bytes(const cgr_gnn_config* cfg, int64_t num_nodes, int64_
 int64_t cgr_gnn_workspace_bytes(const cgr_gnn_config* cfg, int64_t num_nodes, int64_t num_edges,
                                 int64_t num_graphs);
 
-/* Byte offset of a named arena buffer (introspection for tests/debugging).  Names: "status", "rng",
+/* Byte offset of a named arena buffer (introspection for tests/debugging).  "status" is the graph
+ * prep's int32 status word: bit 0 an edge id outside [0, num_nodes), bit 1 an unsorted or
+ * out-of-range batch vector, bit 2 edges not reverse-paired (src(e ^ 1) != dst(e) for some e;
+ * informational: results stay exact, the backward takes its unpaired form).  Names: "status", "rng",
  * "perm", "src_s", "dst_s", "rev_s", "src_list", "dst_ptr", "src_ptr", "graph_ptr",
  * "node_graph", "e_s", "P", "h", "a", "pre", "zn", "hn", "g"; `index` selects the layer for
  * "h" / "a" / "pre".  Returns -1 for an unknown or absent buffer. */
