@@ -8,6 +8,11 @@
 //     vector width VEC in {4, 2, 1} chosen on the host from the leading dimension and alignment.
 #pragma once
 
+#ifndef CGR_HBITS
+#define CGR_HBITS 0  // 1: ReLU masks as bits for the backward (FloatView::hb); A/B -2.4 % (the
+                     // byte stores slow the layer epilogues 2-4 us, the backward did not gain)
+#endif
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

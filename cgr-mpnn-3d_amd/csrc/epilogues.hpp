@@ -156,7 +156,7 @@ struct EpLayer {
         h[k] *= scale;
     }
     *reinterpret_cast<float4*>(hout + o) = make_float4(h[0], h[1], h[2], h[3]);
-    if (hbits)
+    if (CGR_HBITS && hbits)
       hbits[(int64_t)r * (ld >> 2) + (c >> 2)] =
           (uint8_t)((h[0] > 0.f) | ((h[1] > 0.f) << 1) | ((h[2] > 0.f) << 2) | ((h[3] > 0.f) << 3));
   }
@@ -183,7 +183,7 @@ struct EpLayer {
     }
     const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
     *reinterpret_cast<float4*>(hout + o) = hv;
-    if (hbits)
+    if (CGR_HBITS && hbits)
       hbits[(int64_t)r * (ld >> 2) + (c >> 2)] =
           (uint8_t)((h[0] > 0.f) | ((h[1] > 0.f) << 1) | ((h[2] > 0.f) << 2) | ((h[3] > 0.f) << 3));
     return hv;

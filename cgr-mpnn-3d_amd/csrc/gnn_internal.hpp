@@ -72,10 +72,6 @@ struct IndexView {
 #endif
 
 // Forward-saved float state inside the arena.
-#ifndef CGR_HBITS
-#define CGR_HBITS 0  // 1: ReLU masks as bits for the backward (FloatView::hb); A/B -2.4 % (the
-                     // byte stores slow the layer epilogues 2-4 us, the backward did not gain)
-#endif
 struct FloatView {
   float* e_s;   // [E, Fep] sorted, zero padded edge_attr
   float* w0eT;  // [Fe, Hp] transposed edge-feature slice of edge_init.weight

@@ -277,7 +277,7 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
       h.z = act_fwd(z.z, act);
       h.w = act_fwd(z.w, act);
       *reinterpret_cast<float4*>(h0 + o) = h;
-      if (h0bits)
+      if (CGR_HBITS && h0bits)
         h0bits[(int64_t)i * C4 + c] = (uint8_t)((h.x > 0.f) | ((h.y > 0.f) << 1) |
                                                 ((h.z > 0.f) << 2) | ((h.w > 0.f) << 3));
       acc = f4add(acc, h);
@@ -453,6 +453,7 @@ __device__ __forceinline__ void head_bwd_block(const float* __restrict__ dy, con
     hb.dbf[0] = (red[1][0][0] + red[1][1][0]) + (red[1][2][0] + red[1][3][0]);
 }
 
+template <bool HEAD>
 __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dy,
                                                      const float* __restrict__ wf,
                                                      const int* __restrict__ node_graph,
@@ -460,9 +461,11 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
                                                      const float* __restrict__ zn, int64_t N,
                                                      int H, int Hp, int act,
                                                      float* __restrict__ dzn, HeadBwd hb) {
-  if ((int)blockIdx.x >= hb.first_block) {
-    head_bwd_block(dy, hb, (int)blockIdx.x - hb.first_block, H, Hp);
-    return;
+  if constexpr (HEAD) {
+    if ((int)blockIdx.x >= hb.first_block) {
+      head_bwd_block(dy, hb, (int)blockIdx.x - hb.first_block, H, Hp);
+      return;
+    }
   }
   const int C4 = Hp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -509,8 +512,12 @@ hipError_t head_readout_bwd(const float* dy, const float* g, int64_t B, float* d
   const int hbk = dwf ? (int)cdiv(H, 64) : 0;
   if (rb + hbk <= 0) return hipSuccess;
   const HeadBwd hb{g, B, dwf, dbf, rb};
-  hipLaunchKernelGGL(k_readout_bwd, dim3(rb + hbk), dim3(256), 0, st, dy, wf, node_graph, hn, zn,
-                     N, H, Hp, act, dzn, hb);
+  if (hbk)
+    hipLaunchKernelGGL(k_readout_bwd<true>, dim3(rb + hbk), dim3(256), 0, st, dy, wf, node_graph,
+                       hn, zn, N, H, Hp, act, dzn, hb);
+  else
+    hipLaunchKernelGGL(k_readout_bwd<false>, dim3(rb), dim3(256), 0, st, dy, wf, node_graph, hn,
+                       zn, N, H, Hp, act, dzn, hb);
   return hipGetLastError();
 }
 
@@ -542,7 +549,7 @@ __device__ __forceinline__ void kb_planes4(const float (&d)[4], uint16_t* hi_p, 
 // 1 / 0 in m so the consumers test m.k > 0 either way
 __device__ __forceinline__ float4 relu_mask4(const uint8_t* bits, const float* h, int64_t i,
                                              int n, int Hp) {
-  if (bits) {
+  if (CGR_HBITS && bits) {  // (compiled out when off: one load form in the hot kernels)
     const uint32_t b = bits[i * (Hp >> 2) + (n >> 2)];
     return make_float4((float)(b & 1), (float)((b >> 1) & 1), (float)((b >> 2) & 1),
                        (float)((b >> 3) & 1));
@@ -879,7 +886,7 @@ hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int*
 // 16-byte loads instead of 8-byte ones
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_pad_rows(const float* __restrict__ x, int64_t N, int F,
-                                                  float* __restrict__ xp, int ldp) {
+                                                  float* __restrict__ xp, int ldp, int vec2) {
   const int c4n = ldp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * c4n) return;
@@ -887,17 +894,24 @@ __global__ __launch_bounds__(256) void k_pad_rows(const float* __restrict__ x, i
   const int k = 4 * (int)(t - r * c4n);
   const float* src = x + r * F;
   float4 v;
-  v.x = k < F ? src[k] : 0.f;
-  v.y = k + 1 < F ? src[k + 1] : 0.f;
-  v.z = k + 2 < F ? src[k + 2] : 0.f;
-  v.w = k + 3 < F ? src[k + 3] : 0.f;
+  if (vec2) {  // 8-byte-aligned rows (F even): two 8-byte loads (the float2 past F is zeros)
+    const float2 u = k < F ? *reinterpret_cast<const float2*>(src + k) : make_float2(0.f, 0.f);
+    const float2 w = k + 2 < F ? *reinterpret_cast<const float2*>(src + k + 2) : make_float2(0.f, 0.f);
+    v = make_float4(u.x, u.y, w.x, w.y);
+  } else {
+    v.x = k < F ? src[k] : 0.f;
+    v.y = k + 1 < F ? src[k + 1] : 0.f;
+    v.z = k + 2 < F ? src[k + 2] : 0.f;
+    v.w = k + 3 < F ? src[k + 3] : 0.f;
+  }
   *reinterpret_cast<float4*>(xp + r * ldp + k) = v;
 }
 
 hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStream_t st) {
   const int64_t tot = N * (ldp >> 2);
   if (tot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pad_rows, dim3(cdiv(tot, 256)), dim3(256), 0, st, x, N, F, xp, ldp);
+  const int vec2 = (F % 2 == 0) && ((uintptr_t)x & 7) == 0;
+  hipLaunchKernelGGL(k_pad_rows, dim3(cdiv(tot, 256)), dim3(256), 0, st, x, N, F, xp, ldp, vec2);
   return hipGetLastError();
 }
 
