@@ -998,7 +998,9 @@ inline B3TnPlan b3tn_plan(int Nout, int Kout, int R, int target = CGR_B3TN_TARGE
 template <class AL, class BL>
 inline bool b3tn_ok(const AL& al, const BL& bl, int Nout, int R) {
   const int t = (Nout + 15) / 16;
-  const bool shape = t == 25 || t == 32 || t == 8 || t == 3 || t == 2 || t == 6;
+  // (t == 32, H = 512, compiles but runs 3.4x slower than the register-direct fp32 TN there:
+  //  633 vs 186 us per layer weight gradient at cfg5; those shapes take the fp32 kernels)
+  const bool shape = t == 25 || t == 8 || t == 3 || t == 2 || t == 6;
   return shape && B3TnSrc<AL>::fits(al, R) && B3TnSrc<BL>::fits(bl, R);
 }
 // slab bytes the plan needs: splits x Nout x round4(Kout) floats (+ splits x Nout bias)
