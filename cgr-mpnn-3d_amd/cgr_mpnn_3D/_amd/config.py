@@ -7,7 +7,9 @@ import os
 # N' = max(dst) + 1 == num_nodes contract (GNN.py:106 fails with RuntimeError otherwise).
 strict = os.environ.get("CGR_STRICT", "0") not in ("", "0", "false", "False")
 
-# Called with the flat fp32 gradient bucket at the end of every native backward (before the
-# per-parameter views are handed to autograd).  cgr_mpnn_3D._amd.ddp installs an RCCL
-# all-reduce here.
+# Called as hook(flat, buckets, events) after every native backward is enqueued (before the
+# per-parameter views are handed to autograd): flat = the fp32 gradient buffer, buckets = its
+# (start, end) ranges in the order the backward finishes them, events = their ready events (or
+# None; see functional.grad_layout and ddp.GradAllReduce).  cgr_mpnn_3D._amd.ddp installs the
+# RCCL all-reduce here.
 grad_bucket_hook = None

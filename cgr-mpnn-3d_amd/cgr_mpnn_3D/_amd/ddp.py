@@ -1,11 +1,16 @@
-"""Data parallelism over the GPUs of one node: graph-sharded batches + one RCCL all-reduce.
+"""Data parallelism over the GPUs of one node: graph-sharded batches + bucketed RCCL all-reduce.
 
-The reference trains on one device (``train.py:109``).  Reactions are disconnected graphs, so a
-global batch shards by whole reaction graphs with no cross-rank edges; the only
-exchange per step is the gradient sum.  The native backward writes every parameter gradient into
-ONE flat fp32 bucket (``functional.GNNFunction.backward``), so the exchange is a single
-``all_reduce(SUM)`` of 5.9 MB (cfg2) over RCCL/xGMI, issued on the backward's stream before
-autograd hands the per-parameter views to the optimizer.
+The reference trains on one device (``train.py:109-114``, ``trainer.py:138-144``).  Reactions are
+disconnected graphs, so a global batch shards by whole reaction graphs with no cross-rank edges
+(SURVEY.md §8e); the only exchange per step is the gradient sum.  The native backward writes
+every parameter gradient into one flat fp32 buffer laid out in all-reduce bucket order
+(``functional.grad_layout``: edge_to_node + ffn, then the layers from the top down, then
+edge_init + skip weights -- the order in which the backward finishes them) and records a ready
+event per bucket.  ``GradAllReduce`` starts each bucket's ``all_reduce(SUM)`` on a communication
+stream as soon as its event fires, so the collectives of the readout and the upper layers run
+over RCCL/xGMI while the lower layers' backward still computes; the caller's stream then waits
+for the last one before the optimizer reads the gradients.  Everything is stream-ordered (no host
+wait), so the whole step, collectives included, is captured into one HIP graph.
 
 SUM, not AVG: the reference loss is ``MSELoss(reduction="sum")`` (``train.py:120``), so summing
 per-rank gradients reproduces the single-process gradient of the whole global batch.
@@ -18,13 +23,59 @@ import torch
 import torch.distributed as dist
 
 
-def install_grad_allreduce(model, group=None):
-    """Sum the model's flat gradient bucket across `group` inside every native backward."""
+class GradAllReduce:
+    """Bucket hook: ``all_reduce(SUM)`` of every gradient bucket over `group`.
 
-    def hook(flat: torch.Tensor):
-        dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
+    On CUDA tensors with events, bucket b's collective is enqueued on a per-device communication
+    stream after waiting for its ready event (overlapping the rest of the backward), and the
+    caller's stream waits for the communication stream at the end.  Without events (CPU / gloo
+    tests) the buckets are reduced in order on the caller's stream.  `op` replaces the collective
+    (tests: a scaling op shows which bucket ran after which event)."""
 
-    model._grad_bucket_hook = hook
+    def __init__(self, group=None, op=None):
+        self.group = group
+        self.op = op
+        self._streams = {}
+        self._events = {}
+
+    def bucket_events(self, dev, n):
+        key = (dev.index if dev.index is not None else torch.cuda.current_device(), n)
+        evs = self._events.get(key)
+        if evs is None:
+            evs = [torch.cuda.Event() for _ in range(n)]
+            with torch.cuda.device(key[0]):
+                s = torch.cuda.current_stream()
+                for e in evs:  # materialise the hipEvent_t handles (created on first record)
+                    e.record(s)
+            self._events[key] = evs
+        return evs
+
+    def _reduce(self, t):
+        if self.op is not None:
+            self.op(t)
+        else:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def __call__(self, flat, buckets, events):
+        if events is None or not flat.is_cuda:
+            for a, b in buckets:
+                self._reduce(flat[a:b])
+            return
+        dev = flat.device
+        cur = torch.cuda.current_stream(dev)
+        cs = self._streams.get(dev)
+        if cs is None:
+            cs = self._streams[dev] = torch.cuda.Stream(dev)
+        for (a, b), ev in zip(buckets, events):
+            cs.wait_event(ev)
+            with torch.cuda.stream(cs):
+                self._reduce(flat[a:b])
+        cur.wait_stream(cs)
+
+
+def install_grad_allreduce(model, group=None, op=None):
+    """Sum the model's gradient buckets across `group` inside every native backward."""
+    model._grad_bucket_hook = GradAllReduce(group, op)
     return model
 
 

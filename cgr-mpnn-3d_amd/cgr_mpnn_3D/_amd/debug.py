@@ -64,5 +64,5 @@ class ArenaRun:
                 ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
                 _dropout_array(self.dropout_ps, self.cfg.depth), ctypes.c_uint64(self.seed),
                 self.flags, native.ptr(self.arena), native.ptr(dy.contiguous()),
-                _param_table(grads), native.ptr(ws), native.stream_ptr(dev)))
+                _param_table(grads), native.ptr(ws), None, native.stream_ptr(dev)))
         return grads

@@ -46,6 +46,32 @@ def _dropout_array(dropout_ps, depth):
     return arr
 
 
+def grad_layout(shapes, depth):
+    """Flat gradient buffer in all-reduce bucket order (include/cgr_mpnn3d.h, CGR_GRAD_BUCKETS):
+    bucket 0 = edge_to_node + ffn, 1 + k = convs.(depth-1-k), depth + 1 = edge_init + skip
+    weights -- the order in which the native backward finishes them.  Every bucket starts on a
+    16-byte boundary.  `shapes` are the parameter shapes in the C-ABI table order.  Returns
+    (offset of each parameter, [(start, end) of each bucket], total floats)."""
+    D = depth
+    members = [[2 + 2 * D, 3 + 2 * D, 4 + 2 * D, 5 + 2 * D]]
+    members += [[2 + 2 * l, 3 + 2 * l] for l in range(D - 1, -1, -1)]
+    members.append([0, 1] + list(range(6 + 2 * D, len(shapes))))
+    offs = [0] * len(shapes)
+    buckets = []
+    off = 0
+    for mem in members:
+        start = off
+        for i in mem:
+            offs[i] = off
+            n = 1
+            for d in shapes[i]:
+                n *= int(d)
+            off += n
+        buckets.append((start, off))
+        off = (off + 3) // 4 * 4
+    return offs, buckets, off
+
+
 def read_status(arena, cfg, N, E, B) -> int:
     """Graph-prep status word (bit0 bad edge index, bit1 bad/unsorted batch, bit2 edges not
     reverse-paired: informational).  Synchronises."""
@@ -106,25 +132,30 @@ class GNNFunction(torch.autograd.Function):
         dev = x.device
         ws = torch.empty(lib.cgr_gnn_workspace_bytes(ctypes.byref(cfg), N, E, B),
                          dtype=torch.uint8, device=dev)
-        # one flat gradient bucket (ready for a single all-reduce), viewed per parameter
-        numels = [p.numel() for p in params]
-        flat = torch.empty(sum(numels), dtype=torch.float32, device=dev)
-        grads = []
-        off = 0
-        for p, n in zip(params, numels):
-            grads.append(flat[off:off + n].view(p.shape))
-            off += n
+        # one flat gradient buffer in all-reduce bucket order, viewed per parameter
+        offs, buckets, total = grad_layout([tuple(p.shape) for p in params], cfg.depth)
+        flat = torch.empty(total, dtype=torch.float32, device=dev)
+        grads = [flat[o:o + p.numel()].view(p.shape) for o, p in zip(offs, params)]
         dy = dy.contiguous().float()
         bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
+        hook = ctx.bucket_hook if ctx.bucket_hook is not None else _config.grad_bucket_hook
+        # per-bucket ready events (recorded by the native backward) when the hook wants them
+        events = None
+        if hook is not None and hasattr(hook, "bucket_events"):
+            events = hook.bucket_events(dev, len(buckets))
+        evtab = None
+        if events is not None:
+            evtab = (c_void_p * len(events))(*[e.cuda_event for e in events])
         with native.device_guard(dev):
             native.check(lib.cgr_gnn_backward(
                 ctypes.byref(cfg), _param_table(params), ctypes.byref(bs),
                 _dropout_array(ctx.dropout_ps, cfg.depth), ctypes.c_uint64(ctx.seed),
                 ctx.flags, native.ptr(arena), native.ptr(dy), _param_table(grads),
-                native.ptr(ws), native.stream_ptr(dev)))
-        hook = ctx.bucket_hook if ctx.bucket_hook is not None else _config.grad_bucket_hook
+                native.ptr(ws), evtab, native.stream_ptr(dev)))
         if hook is not None:
-            hook(flat)  # e.g. RCCL all-reduce of the whole bucket (cgr_mpnn_3D._amd.ddp)
+            # e.g. the RCCL all-reduce of every bucket, each started as soon as its event fires
+            # (cgr_mpnn_3D._amd.ddp); must leave the current stream ordered after its work
+            hook(flat, buckets, events)
         return (None,) * 12 + tuple(grads)
 
 

@@ -15,7 +15,7 @@ _LIB_NAME = "libcgr_mpnn3d.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CGR_MPNN3D_LIB", os.path.join(_HERE, "lib", _LIB_NAME))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 TRAIN_DROPOUT, TRAIN_FOR_BACKWARD = 1, 2  # cgr_gnn_forward / _backward `training` bits
 MAX_DEPTH = 32
 ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
@@ -75,7 +75,7 @@ SIGNATURES = [
       c_void_p, c_int32, c_void_p, c_void_p, c_void_p]),
     ("cgr_gnn_backward", c_int32,
      [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
-      c_int32, c_void_p, c_void_p, POINTER(c_void_p), c_void_p, c_void_p]),
+      c_int32, c_void_p, c_void_p, POINTER(c_void_p), c_void_p, POINTER(c_void_p), c_void_p]),
     ("cgr_segment_sum", c_int32,
      [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
     ("cgr_dmpnn_conv_scratch_bytes", c_int64, [c_int64, c_int64, c_int64]),

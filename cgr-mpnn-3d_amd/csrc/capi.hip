@@ -2,7 +2,10 @@
 // reporting.  No entry point allocates or synchronises; all work is enqueued on `stream`.
 #include <string.h>
 
+#include <algorithm>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 
 #include "dispatch.hpp"
 #include "gnn_internal.hpp"
@@ -13,12 +16,29 @@ namespace cgr {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 
+// `training` bits of the forward that last filled each arena (host side, so the check costs no
+// device sync and holds under graph capture): the backward needs the W^T images that only a
+// CGR_TRAIN_FOR_BACKWARD forward packs.  Keys are arena addresses; the caching allocator reuses
+// them, so the table stays as small as the set of live arena blocks.
+static std::mutex g_arena_mu;
+static std::unordered_map<const void*, int> g_arena_flags;
+static void note_forward(const void* arena, int flags) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  g_arena_flags[arena] = flags;
+}
+static int forward_flags(const void* arena) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  const auto it = g_arena_flags.find(arena);
+  return it == g_arena_flags.end() ? -1 : it->second;
+}
+
 int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
                      const float* dropout_p, uint64_t seed, uint64_t* rng_counter, int training,
                      void* arena, float* y, hipStream_t st);
 int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
                       const float* dropout_p, uint64_t seed, int training, const void* arena,
-                      const float* dy, float* const* grads, void* workspace, hipStream_t st);
+                      const float* dy, float* const* grads, void* workspace,
+                      hipEvent_t const* bucket_events, hipStream_t st);
 
 Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
   Dims d;
@@ -82,32 +102,17 @@ ArenaLayout arena_layout(const Dims& d) {
   L.P = b.take(4 * N * Hp);
   L.Q = b.take(4 * N * Hp);
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
-  L.wT = CGR_B3 ? kNone : b.take(4 * (size_t)(d.D + 1) * d.H * Hp);
-  if (CGR_B3) {
-    // x-GEMM images: one of 2H rows, or (split x-GEMM) two of H rows back to back
-    const size_t xi = std::max(b3_img_u4(2 * d.H, d.F), 2 * b3_img_u4(d.H, d.F));
-    L.b3x = d.F > 0 ? b.take(16 * xi) : kNone;
-    L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
-    L.b3rob = b.take(16 * b3_img_u4(d.H, d.H));
-    for (int l = 0; l < d.D; ++l) {
-      L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
-      L.b3lb[l] = b.take(16 * b3_img_u4(d.H, d.H));
-    }
-    if (CGR_B3TP) {
-      const size_t pb = 2 * (size_t)b3tp_rows(d.E) * (size_t)b3tp_layer_ld(d.H);
-      for (int l = 0; l < d.D; ++l) {
-        L.mhi[l] = b.take(pb);
-        L.mlo[l] = b.take(pb);
-      }
-    }
+  L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
+  L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
+  L.b3rob = b.take(16 * b3_img_u4(d.H, d.H));
+  for (int l = 0; l < d.D; ++l) {
+    L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
+    L.b3lb[l] = b.take(16 * b3_img_u4(d.H, d.H));
   }
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
     L.a[l] = l <= d.D ? b.take(4 * N * Hp) : kNone;
     L.pre[l] = (l <= d.D && d.act != CGR_ACT_RELU) ? b.take(4 * E * Hp) : kNone;
-    // h_0's mask comes from the fused edge init (Hp <= 512), every layer's from its epilogue
-    L.hb[l] = (CGR_HBITS && l <= d.D && d.act == CGR_ACT_RELU && (l > 0 || Hp <= 512))
-                  ? b.take(E * (Hp / 4)) : kNone;
   }
   L.zn = d.act != CGR_ACT_RELU ? b.take(4 * N * Hp) : kNone;
   L.hn = b.take(4 * N * Hp);
@@ -154,32 +159,20 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.P = (float*)at(arena, L.P);
   f.Q = (float*)at(arena, L.Q);
   f.xp = (float*)at(arena, L.xp);
-  f.wT = (float*)at(arena, L.wT);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     f.h[l] = (float*)at(arena, L.h[l]);
     f.a[l] = (float*)at(arena, L.a[l]);
     f.pre[l] = (float*)at(arena, L.pre[l]);
-    f.hb[l] = (uint8_t*)at(arena, L.hb[l]);
   }
   f.zn = (float*)at(arena, L.zn);
   f.hn = (float*)at(arena, L.hn);
   f.g = (float*)at(arena, L.g);
-  f.b3x = f.b3rof = f.b3rob = nullptr;
-  for (int l = 0; l < CGR_MAX_DEPTH; ++l) f.b3lf[l] = f.b3lb[l] = nullptr;
-  for (int l = 0; l < CGR_MAX_DEPTH; ++l) f.mhi[l] = f.mlo[l] = nullptr;
-  f.mld = b3tp_layer_ld(d.H);
-  if (CGR_B3) {
-    f.b3x = at(arena, L.b3x);
-    f.b3rof = at(arena, L.b3rof);
-    f.b3rob = at(arena, L.b3rob);
-    for (int l = 0; l < d.D; ++l) {
-      f.b3lf[l] = at(arena, L.b3lf[l]);
-      f.b3lb[l] = at(arena, L.b3lb[l]);
-      if (CGR_B3TP) {
-        f.mhi[l] = static_cast<uint16_t*>(at(arena, L.mhi[l]));
-        f.mlo[l] = static_cast<uint16_t*>(at(arena, L.mlo[l]));
-      }
-    }
+  f.b3x = at(arena, L.b3x);
+  f.b3rof = at(arena, L.b3rof);
+  f.b3rob = at(arena, L.b3rob);
+  for (int l = 0; l < CGR_MAX_DEPTH; ++l) {
+    f.b3lf[l] = l < d.D ? at(arena, L.b3lf[l]) : nullptr;
+    f.b3lb[l] = l < d.D ? at(arena, L.b3lb[l]) : nullptr;
   }
   return f;
 }
@@ -187,114 +180,47 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
 WorkspaceLayout workspace_layout(const Dims& d) {
   WorkspaceLayout W;
   Bump b;
-  const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
-  for (int l = 0; l < (CGR_DPRE_RING ? 2 : d.D); ++l) W.dpre[l] = b.take(4 * E * Hp);
-  for (int l = 0; l < CGR_MAX_DEPTH; ++l) W.dphi[l] = W.dplo[l] = (size_t)-1;
-  if (CGR_B3 && CGR_B3TP) {
-    const size_t pb = 2 * (size_t)b3tp_rows(d.E) * (size_t)b3tp_layer_ld(d.H);
-    for (int l = 0; l < (CGR_DPRE_RING ? 2 : d.D); ++l) {
-      W.dphi[l] = b.take(pb);
-      W.dplo[l] = b.take(pb);
-    }
-  }
+  const size_t N = (size_t)d.N, E = (size_t)d.E, Hp = (size_t)d.Hp;
+  for (int l = 0; l < 2; ++l) W.dpre[l] = b.take(4 * E * Hp);
   W.dm = b.take(4 * E * Hp);
   W.dh0 = b.take(4 * E * Hp);
   W.dzn = b.take(4 * N * Hp);
   W.ds = b.take(4 * N * Hp);
   W.Gs = b.take(4 * N * Hp);
-  W.dg = b.take(4 * B * Hp);
+  // split-K slabs: every plan a call site may pick for its shape (gnn_bwd.hip), the largest wins.
+  // The side-stream weight gradients (readout, layers, edge features) run one after another and
+  // share `slab`; the node weight gradient runs beside them on the caller's stream: `slab2`.
   size_t slab = 0, bslab = 0;
-  auto acc = [&](int Nout, int Kout, int64_t R) {
-    const TnPlan p = tn_plan(Nout, Kout, (int)R);
-    const size_t s = (size_t)p.splits * Nout * (size_t)((Kout + 3) & ~3);  // rows padded to 4
-    const size_t bs = (size_t)p.splits * Nout;
-    slab = s > slab ? s : slab;
-    bslab = bs > bslab ? bs : bslab;
+  auto fit = [&](const TnPlan& p, int Nout, int Kout) {
+    slab = std::max(slab, (size_t)p.splits * Nout * (size_t)((Kout + 3) & ~3));  // rows to 4
+    bslab = std::max(bslab, (size_t)p.splits * Nout);
   };
-  // side-stream TN GEMMs (readout, layers, edge features): with batched reduction each gets its
-  // own slab (reduced together in one launch at the end of the side stream), otherwise they share
-  // one; the main-stream TN (x-part of edge init) runs beside them and always gets its own
-  auto side = [&](int Nout, int Kout, int64_t R) {
-    if (!CGR_BATCH_REDUCE) return acc(Nout, Kout, R);
-    const TnPlan p = tn_plan(Nout, Kout, (int)R);
-    slab += (size_t)p.splits * Nout * (size_t)((Kout + 3) & ~3);
-    bslab += (size_t)p.splits * Nout;
-  };
-  side(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N);  // readout TN runs over [xp | s] when padded
-  if (!CGR_BATCH_REDUCE) {  // register-direct readout TN: its own split count
-    const int Kr = (d.F % 4 ? d.Fp : d.F) + d.H;
-    const TnrPlan q = plan_tnr<5, 4>(d.H, Kr, (int)d.N, CGR_TNR_RO_TARGET);
-    const size_t s2 = (size_t)q.splits * d.H * (size_t)((Kr + 3) & ~3), bs2 = (size_t)q.splits * d.H;
-    slab = s2 > slab ? s2 : slab;
-    bslab = bs2 > bslab ? bs2 : bslab;
-  }
-  auto b3acc = [&](int Nout, int Kout, int64_t R, int copies,
-                   int target = CGR_B3TN_TARGET) {  // split-bf16 TN plans
-    if (!CGR_B3TN) return;
-    const TnPlan q = b3tn_tnplan(Nout, Kout, (int)R, target);
-    const size_t s = (size_t)q.splits * Nout * (size_t)((Kout + 3) & ~3);
-    const size_t bs = (size_t)q.splits * Nout;
-    if (CGR_BATCH_REDUCE) {
-      slab += (size_t)copies * s;  // (over-allocates, as below)
-      bslab += (size_t)copies * bs;
-    } else {
-      slab = s > slab ? s : slab;
-      bslab = bs > bslab ? bs : bslab;
-    }
-  };
-  b3acc(d.H, (d.F % 4 ? d.Fp : d.F) + d.H, d.N, 1, CGR_B3TN_RO_TARGET);
-  b3acc(d.H, d.H, d.E, d.D);
-  if (CGR_B3 && CGR_B3TP) {  // plane TN plans of the layer weight gradients
-    const B3TpPlan q = b3tp_plan(d.H, d.H, (int)d.E);
-    const size_t s = (size_t)q.splits * d.H * (size_t)((d.H + 3) & ~3), bs = (size_t)q.splits * d.H;
-    if (CGR_BATCH_REDUCE) {
-      slab += (size_t)d.D * s;
-      bslab += (size_t)d.D * bs;
-    } else {
-      slab = s > slab ? s : slab;
-      bslab = bs > bslab ? bs : bslab;
-    }
-  }
-  for (int l = 0; l < (CGR_BATCH_REDUCE ? d.D : 1); ++l) side(d.H, d.H, d.E);
-  {  // the layer weight gradient may run on the register-direct kernel with its own split count
+  auto tnr = [&](const TnrPlan& q) { return TnPlan{q.tiles_n, q.tiles_k, q.splits, q.rows_per_split}; };
+  const int Fx = d.F % 4 ? d.Fp : d.F;  // x columns the x-side GEMMs cover (pad columns zero)
+  const int Kr = Fx + d.H;              // readout: [x | s]
+  fit(tn_plan(d.H, Kr, (int)d.N), d.H, Kr);
+  fit(tnr(plan_tnr<5, 4>(d.H, Kr, (int)d.N, kTnrReadoutTarget)), d.H, Kr);
+  fit(b3tn_tnplan(d.H, Kr, (int)d.N, kB3TnReadoutTarget), d.H, Kr);
+  fit(tn_plan(d.H, d.H, (int)d.E), d.H, d.H);
+  fit(b3tn_tnplan(d.H, d.H, (int)d.E), d.H, d.H);
+  {
     const int tf = tnr_layer_frags(d.H);
-    const TnrPlan q = tf == 5   ? plan_tnr<5, 5>(d.H, d.H, (int)d.E, CGR_TNR_TARGET_WGS)
-                      : tf == 4 ? plan_tnr<4, 4>(d.H, d.H, (int)d.E, CGR_TNR_TARGET_WGS)
-                                : TnrPlan{0, 0, 0, 0};
-    const size_t s = (size_t)q.splits * d.H * (size_t)((d.H + 3) & ~3);
-    const size_t bs = (size_t)q.splits * d.H;
-    if (CGR_BATCH_REDUCE) {
-      slab += (size_t)d.D * s;  // (over-allocates: both sizes counted; batching is an A/B option)
-      bslab += (size_t)d.D * bs;
-    } else {
-      slab = s > slab ? s : slab;
-      bslab = bs > bslab ? bs : bslab;
-    }
+    if (tf == 5) fit(tnr(plan_tnr<5, 5>(d.H, d.H, (int)d.E, kTnrLayerTarget)), d.H, d.H);
+    if (tf == 4) fit(tnr(plan_tnr<4, 4>(d.H, d.H, (int)d.E, kTnrLayerTarget)), d.H, d.H);
   }
-  if (d.Fe > 0) side(d.H, d.Fe, d.E);
+  if (d.Fe > 0) fit(tn_plan(d.H, d.Fe, (int)d.E, kEdgeTnTargetWorkgroups), d.H, d.Fe);
   W.slab_elems = slab;
   W.bslab_elems = bslab;
-  W.slab = b.take(4 * slab);
-  W.bslab = b.take(4 * bslab);
-  slab = 0;
-  bslab = 0;
+  W.slab = b.take(4 * std::max<size_t>(slab, 1));
+  W.bslab = b.take(4 * std::max<size_t>(bslab, 1));
+  slab = bslab = 0;
   if (d.F > 0) {
-    acc(d.H, d.F, d.N);
-    const int Fx = d.F % 4 ? d.Fp : d.F;  // register-direct node TN covers the padded columns
-    const TnrPlan q = plan_tnr<5, 4>(d.H, Fx, (int)d.N, CGR_TNR_NODE_TARGET);
-    const size_t s2 = (size_t)q.splits * d.H * (size_t)((Fx + 3) & ~3), bs2 = (size_t)q.splits * d.H;
-    slab = s2 > slab ? s2 : slab;
-    bslab = bs2 > bslab ? bs2 : bslab;
-    if (CGR_B3TN) {
-      const TnPlan b3 = b3tn_tnplan(d.H, Fx, (int)d.N, CGR_B3TN_NODE_TARGET);
-      const size_t s3 = (size_t)b3.splits * d.H * (size_t)((Fx + 3) & ~3), bs3 = (size_t)b3.splits * d.H;
-      slab = s3 > slab ? s3 : slab;
-      bslab = bs3 > bslab ? bs3 : bslab;
-    }
+    fit(tn_plan(d.H, d.F, (int)d.N), d.H, d.F);
+    fit(tnr(plan_tnr<5, 4>(d.H, Fx, (int)d.N, kTnrNodeTarget)), d.H, Fx);
+    fit(b3tn_tnplan(d.H, Fx, (int)d.N, kB3TnNodeTarget), d.H, Fx);
   }
-  if (d.Fe > 0) acc(d.H, d.Fe, d.E);  // the edge-feature TN may use slab2 (CGR_EDGE_TN_MAIN)
-  W.slab2 = b.take(4 * (slab > 0 ? slab : 1));
-  W.bslab2 = b.take(4 * (bslab > 0 ? bslab : 1));
+  W.slab2 = b.take(4 * std::max<size_t>(slab, 1));
+  W.bslab2 = b.take(4 * std::max<size_t>(bslab, 1));
   W.dsig_blocks = segsum_act_bwd_blocks(d.E, d.N, d.Hp);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
   W.bytes = b.off;
@@ -407,16 +333,22 @@ int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params, const
   if (rc) return rc;
   CGR_CHECK(params != nullptr && arena != nullptr && y != nullptr,
             "cgr: params / arena / y must not be NULL");
+  CGR_CHECK((training & ~(CGR_TRAIN_DROPOUT | CGR_TRAIN_FOR_BACKWARD)) == 0,
+            "cgr: unknown `training` bits (CGR_TRAIN_DROPOUT | CGR_TRAIN_FOR_BACKWARD)");
   const int np = cgr_gnn_num_params(cfg);
   for (int i = 0; i < np; ++i) CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
   const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
-  return gnn_forward_impl(d, params, b, dropout_p, seed, rng_counter, training, arena, y,
-                          (hipStream_t)stream);
+  note_forward(arena, -1);  // not usable by a backward unless the forward below succeeds
+  const int r = gnn_forward_impl(d, params, b, dropout_p, seed, rng_counter, training, arena, y,
+                                 (hipStream_t)stream);
+  if (r == 0) note_forward(arena, training);
+  return r;
 }
 
 int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,
                      const float* dropout_p, uint64_t seed, int32_t training, const void* arena,
-                     const float* dy, float* const* grads, void* workspace, void* stream) {
+                     const float* dy, float* const* grads, void* workspace,
+                     void* const* bucket_events, void* stream) {
   clear_stale_hip_error();
   int rc = validate_config(cfg);
   if (rc) return rc;
@@ -425,13 +357,25 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, cons
   CGR_CHECK(params != nullptr && arena != nullptr && dy != nullptr && grads != nullptr &&
                 workspace != nullptr,
             "cgr: params / arena / dy / grads / workspace must not be NULL");
+  CGR_CHECK((training & ~(CGR_TRAIN_DROPOUT | CGR_TRAIN_FOR_BACKWARD)) == 0,
+            "cgr: unknown `training` bits (CGR_TRAIN_DROPOUT | CGR_TRAIN_FOR_BACKWARD)");
+  const int ff = forward_flags(arena);
+  CGR_CHECK(ff >= 0 && (ff & CGR_TRAIN_FOR_BACKWARD),
+            "cgr_gnn_backward: `arena` was not filled by a successful cgr_gnn_forward with "
+            "CGR_TRAIN_FOR_BACKWARD set");
+  CGR_CHECK((ff & CGR_TRAIN_DROPOUT) == (training & CGR_TRAIN_DROPOUT),
+            "cgr_gnn_backward: `training` dropout bit differs from the forward's");
   const int np = cgr_gnn_num_params(cfg);
   for (int i = 0; i < np; ++i) {
     CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
     CGR_CHECK(grads[i] != nullptr, "cgr: NULL gradient pointer");
   }
   const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
+  if (bucket_events)
+    for (int i = 0; i < CGR_GRAD_BUCKETS(cfg->depth); ++i)
+      CGR_CHECK(bucket_events[i] != nullptr, "cgr_gnn_backward: NULL bucket event");
   return gnn_backward_impl(d, params, b, dropout_p, seed, training, arena, dy, grads, workspace,
+                           reinterpret_cast<hipEvent_t const*>(bucket_events),
                            (hipStream_t)stream);
 }
 

@@ -8,13 +8,10 @@
 //     vector width VEC in {4, 2, 1} chosen on the host from the leading dimension and alignment.
 #pragma once
 
-#ifndef CGR_HBITS
-#define CGR_HBITS 0  // 1: ReLU masks as bits for the backward (FloatView::hb); A/B -2.4 % (the
-                     // byte stores slow the layer epilogues 2-4 us, the backward did not gain)
-#endif
-
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <atomic>
 
 namespace cgr {
 
@@ -134,6 +131,22 @@ __device__ __forceinline__ float f4get(const float4& v, int i) {
 
 __host__ __device__ inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 __host__ __device__ inline int64_t cdiv(int64_t x, int64_t m) { return (x + m - 1) / m; }
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): one static per
+// launch-template instantiation, a bit per device ordinal, safe from several host threads
+struct LdsLimit {
+  std::atomic<uint64_t> done{0};
+  hipError_t ensure(const void* kern, int bytes) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    const uint64_t bit = 1ull << (dev & 63);
+    if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+    e = hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done.fetch_or(bit, std::memory_order_acq_rel);
+    return e;
+  }
+};
 
 // Wave-level sum (64 lanes).
 __device__ __forceinline__ float wave_sum(float v) {

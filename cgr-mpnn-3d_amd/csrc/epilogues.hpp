@@ -11,9 +11,6 @@ struct EpStore {
   int64_t ld;
   int M, N;
   const float* bias;
-  __device__ __forceinline__ void operator()(int r, int c, float v) const {
-    if (r < M && c < N) C[(int64_t)r * ld + c] = bias ? v + bias[c] : v;
-  }
   // c % 4 == 0; columns >= N are dropped (ld >= round_up(N, 4) for internal buffers)
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
     if (r >= M || c >= N) return;
@@ -42,12 +39,6 @@ struct EpStore {
     if (!bias) return f4zero();
     return make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
                        bias[min(c + 3, N - 1)]);
-  }
-  // scalar form (row-stationary kernel: one accumulator element per call)
-  typedef float Pre1;
-  __device__ __forceinline__ Pre1 pre1(int r, int c) const { return bias ? bias[min(c, N - 1)] : 0.f; }
-  __device__ __forceinline__ void apply1p(int r, int c, float v, Pre1 b, const Ctx&) const {
-    if (r < M && c < N) C[(int64_t)r * ld + c] = v + b;
   }
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& b, const Ctx&) const {
     if (r >= M || c >= N) return;
@@ -79,19 +70,6 @@ struct EpLayer {
   float scale;      // 1 / (1 - p)
   const uint64_t* seed;  // device: the forward's dropout key (arena "rng"); read iff thresh
   int layer;
-  uint8_t* hbits = nullptr;  // [M, ld/4] masks h > 0 (4 bits per float4; apply4p paths only)
-  __device__ __forceinline__ void operator()(int r, int c, float v) const {
-    if (r >= M || c >= N) return;
-    const int64_t o = (int64_t)r * ld + c;
-    const float sg = sigma ? sigma[0] : 1.f;
-    const float z = (v + bias[c]) + sg * h0[o];
-    if (pre) pre[o] = z;
-    float h = act_fwd(z, act);
-    if (thresh) h = drop_keep(*seed, (uint32_t)layer, (uint64_t)r * N + c, thresh) ? h * scale : 0.f;
-
-    else h *= scale;
-    hout[o] = h;
-  }
   // internal [M, ld] buffers, ld % 4 == 0: whole float4 in bounds of the padded row; columns >= N
   // hold don't-care values (never read as data)
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
@@ -115,26 +93,6 @@ struct EpLayer {
                make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
                            bias[min(c + 3, N - 1)])};
   }
-  struct Pre1 {
-    float h0, b;
-  };
-  __device__ __forceinline__ Pre1 pre1(int r, int c) const {
-    const bool ok = r < M && c < N;
-    return Pre1{h0[ok ? (int64_t)r * ld + c : 0], bias[min(c, N - 1)]};
-  }
-  __device__ __forceinline__ void apply1p(int r, int c, float v, const Pre1& p,
-                                          const Ctx& cx) const {
-    if (r >= M || c >= N) return;
-    const int64_t o = (int64_t)r * ld + c;
-    const float z = (v + p.b) + cx.sg * p.h0;
-    if (pre) pre[o] = z;
-    float h = act_fwd(z, act);
-    if (thresh)
-      h = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c, thresh) ? h * scale : 0.f;
-    else
-      h *= scale;
-    hout[o] = h;
-  }
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& p,
                                           const Ctx& cx) const {
     if (r >= M || c >= N) return;
@@ -156,49 +114,7 @@ struct EpLayer {
         h[k] *= scale;
     }
     *reinterpret_cast<float4*>(hout + o) = make_float4(h[0], h[1], h[2], h[3]);
-    if (CGR_HBITS && hbits)
-      hbits[(int64_t)r * (ld >> 2) + (c >> 2)] =
-          (uint8_t)((h[0] > 0.f) | ((h[1] > 0.f) << 1) | ((h[2] > 0.f) << 2) | ((h[3] > 0.f) << 3));
   }
-  // apply4p that also returns the stored values (rows / columns outside: v unchanged)
-  __device__ __forceinline__ float4 apply4p_h(int r, int c, float4 v, const Pre& p,
-                                              const Ctx& cx) const {
-    if (r >= M || c >= N) return v;
-    const int64_t o = (int64_t)r * ld + c;
-    float z[4] = {v.x, v.y, v.z, v.w};
-    const float h0v[4] = {p.h0.x, p.h0.y, p.h0.z, p.h0.w};
-    const float bv[4] = {p.b.x, p.b.y, p.b.z, p.b.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) z[k] = (z[k] + bv[k]) + cx.sg * h0v[k];
-    if (pre) *reinterpret_cast<float4*>(pre + o) = make_float4(z[0], z[1], z[2], z[3]);
-    float h[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      h[k] = act_fwd(z[k], act);
-      if (thresh)
-        h[k] = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
-                                                                                    : 0.f;
-      else
-        h[k] *= scale;
-    }
-    const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
-    *reinterpret_cast<float4*>(hout + o) = hv;
-    if (CGR_HBITS && hbits)
-      hbits[(int64_t)r * (ld >> 2) + (c >> 2)] =
-          (uint8_t)((h[0] > 0.f) | ((h[1] > 0.f) << 1) | ((h[2] > 0.f) << 2) | ((h[3] > 0.f) << 3));
-    return hv;
-  }
-};
-
-// EpLayer whose GEMM also produces the layer's scatter-add a[v] = sum_{dst(e) = v} h'[e]
-// (GNN.py:134) for the dst segments lying wholly inside its row tile (rows are dst-sorted):
-// the tile's h' goes back through LDS and each segment is summed in row order, the order of
-// k_segsum_v4 (bitwise the unfused result).  Segments crossing a tile boundary and empty ones
-// are left to segsum_fixup (kernels.hip).
-struct EpLayerSeg : EpLayer {
-  const int* dst_s;  // [M] node of each (dst-sorted) row
-  float* aout;       // [nodes, lda]
-  int64_t lda;
 };
 
 // merged x-GEMM output [N, 2H]: columns [0, H) -> P (edge-init half), [H, 2H) -> Q (readout's
@@ -276,13 +192,6 @@ struct EpReadout {
   int64_t ld;
   int M, N;
   int act;
-  __device__ __forceinline__ void operator()(int r, int c, float v) const {
-    if (r >= M || c >= N) return;
-    const int64_t o = (int64_t)r * ld + c;
-    const float z = v + bias[c];
-    if (zn) zn[o] = z;
-    hn[o] = act_fwd(z, act);
-  }
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
     if (r >= M || c >= N) return;
     const int64_t o = (int64_t)r * ld + c;

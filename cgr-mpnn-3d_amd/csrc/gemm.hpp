@@ -261,9 +261,9 @@ struct NTShape {
   static_assert(ACH % NT == 0, "A chunks per thread must be integral");
 };
 
-#ifndef CGR_NT_IL
-#define CGR_NT_IL 5  // lab: layer NT gather 65.7 -> 59.0 us, plain 58.3 -> 53.8; step A/B -2 % (4: -1.5 %)
-#endif
+// the next tile's global loads spread over the MFMAs, one per kNtIl (lab: layer NT gather 65.7 ->
+// 59.0 us, plain 58.3 -> 53.8; step A/B -2 %; 4: -1.5 %)
+constexpr int kNtIl = 5;
 // OCC > 0 asks the compiler for OCC waves per SIMD (register budget 512 / OCC per lane)
 template <int WAVES, int RM, int RN, int KT, int PF, int OCC, class AL, class BL, class EP>
 __global__ __attribute__((amdgpu_flat_work_group_size(1, WAVES * 64),
@@ -380,28 +380,24 @@ gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int K, int tiles_n) {
     sstore(ra, rb, 0, 0);
     __syncthreads();
     int kt = 0;
-    // CGR_NT_IL > 0: the loads of tile t+2 are spread over tile t's MFMAs (one per CGR_NT_IL)
-    // instead of issued as one burst ahead of them
+    // the loads of tile t+2 are spread over tile t's MFMAs (one per kNtIl) instead of issued as
+    // one burst ahead of them
     auto il = [&]() {
-      if constexpr (CGR_NT_IL > 0) {
-        __builtin_amdgcn_sched_group_barrier(0x100, KT * (RM + RN), 0);  // fragment ds_reads
+      __builtin_amdgcn_sched_group_barrier(0x100, KT * (RM + RN), 0);  // fragment ds_reads
 #pragma unroll
-        for (int q = 0; q < APT * (sizeof(typename AL::Raw) / 16) + BPT; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, CGR_NT_IL, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        }
+      for (int q = 0; q < APT * (sizeof(typename AL::Raw) / 16) + BPT; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x008, kNtIl, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
       }
     };
     for (; kt + 2 <= nk; kt += 2) {  // buf 0 holds tile kt, set 2 holds tile kt + 1
       fetch(ra, rb, (kt + 2) * BK);
-      if constexpr (CGR_NT_IL == 0) __builtin_amdgcn_sched_barrier(0);  // loads ahead of MFMAs
       compute(0);
       il();
       __builtin_amdgcn_sched_barrier(0);
       sstore(ra2, rb2, 1, (kt + 1) * BK);
       __syncthreads();
       fetch(ra2, rb2, (kt + 3) * BK);
-      if constexpr (CGR_NT_IL == 0) __builtin_amdgcn_sched_barrier(0);
       compute(1);
       il();
       __builtin_amdgcn_sched_barrier(0);
@@ -482,12 +478,6 @@ struct TNShape {
   static_assert(ACH % NT == 0, "A chunks per thread must be integral");
 };
 
-#ifndef CGR_TN_IL
-#define CGR_TN_IL 0  // interleaved loads in the LDS-staged TN: A/B neutral (readout TN 106 us either way)
-#endif
-#ifndef CGR_TN_FRAG_FIRST
-#define CGR_TN_FRAG_FIRST 0
-#endif
 template <int WAVES, int RM, int RN, int KT, class AL, class BL, int PF>
 __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
     AL al, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout, int R,
@@ -581,28 +571,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
   auto compute = [&](int cur) {
     const float* Ab = At + cur * BE * SA;
     const float* Bb = Bt + cur * BE * SB;
-#if CGR_TN_FRAG_FIRST
-    // every fragment of the k-tile is read from LDS before the MFMAs (hipcc otherwise issues one
-    // ds_read2 pair per two MFMAs and waits lgkmcnt right before each, exposing LDS latency)
-    float av[4 * KT][RM], bv[4 * KT][RN];
-#pragma unroll
-    for (int s = 0; s < 4 * KT; ++s) {
-      const int er = 4 * s + fg;
-#pragma unroll
-      for (int i = 0; i < RM; ++i) av[s][i] = Ab[er * SA + w * 16 * RM + i * 16 + fr];
-#pragma unroll
-      for (int j = 0; j < RN; ++j) bv[s][j] = Bb[er * SB + j * 16 + fr];
-    }
-#pragma unroll
-    for (int s = 0; s < 4 * KT; ++s)
-#pragma unroll
-      for (int i = 0; i < RM; ++i)
-#pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[s][i], bv[s][j], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_sched_group_barrier(0x100, 4 * KT * (RM + RN), 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, 4 * KT * RM * RN, 0);
-#else
 #pragma unroll
     for (int s = 0; s < 4 * KT; ++s) {
       const int er = 4 * s + fg;
@@ -617,7 +585,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
     }
-#endif
     if (do_bias) {
 #pragma unroll
       for (int e = 0; e < BE; ++e) bsum += Ab[e * SA + tid];
@@ -633,36 +600,16 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_tn_kernel(
       sstore(x, 0);
     }
     __syncthreads();
-    if constexpr (CGR_TN_IL > 0) {
-      // branch-free: tiles past the split fetch in-bounds rows masked by combine (and land in the
-      // idle buffer), so the next tile's loads can be spread over this tile's MFMAs
-      for (int t = 0; t < nt; ++t) {
-        const int cur = t & 1;
-        fetch(x);
-        mkrows(t + 2);
-        compute(cur);
-        __builtin_amdgcn_sched_group_barrier(0x100, 4 * KT * (RM + RN), 0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, CGR_TN_IL, 0);
-          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        sstore(x, cur ^ 1);
-        __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const int cur = t & 1;
+      const bool more = t + 1 < nt;
+      if (more) {
+        fetch(x);       // tile t+1, rows prepared during the previous iteration
+        mkrows(t + 2);  // index loads for tile t+2
       }
-    } else {
-      for (int t = 0; t < nt; ++t) {
-        const int cur = t & 1;
-        const bool more = t + 1 < nt;
-        if (more) {
-          fetch(x);       // tile t+1, rows prepared during the previous iteration
-          mkrows(t + 2);  // index loads for tile t+2
-        }
-        compute(cur);
-        if (more) sstore(x, cur ^ 1);
-        __syncthreads();
-      }
+      compute(cur);
+      if (more) sstore(x, cur ^ 1);
+      __syncthreads();
     }
   } else if (nt > 0) {
     // prefetch distance 2: tile t+2 is fetched before tile t is computed and written to LDS at
@@ -745,10 +692,9 @@ inline TnPlan plan_tn(int Nout, int Kout, int R, int target_wgs) {
   return p;
 }
 
-#ifndef CGR_TN_PF
-#define CGR_TN_PF 1  // 2: same-box A/B +1% step time (layer wgrad slower, node/readout faster)
-#endif
-template <int WAVES, int RM, int RN, int KT, class AL, class BL, int PF = CGR_TN_PF>
+// TN prefetch distance (2: same-box A/B +1 % step time, layer wgrad slower, node/readout faster)
+constexpr int kTnPf = 1;
+template <int WAVES, int RM, int RN, int KT, class AL, class BL, int PF = kTnPf>
 inline hipError_t launch_gemm_tn(const AL& al, const BL& bl, const TnPlan& p, float* slab,
                                  float* bslab, int Nout, int Kout, int R, bool want_bias,
                                  hipStream_t st) {

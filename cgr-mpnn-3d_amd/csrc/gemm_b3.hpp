@@ -184,29 +184,11 @@ struct B3NtShape {
   static constexpr int BPT = (BU4 + NT - 1) / NT;
   static constexpr int LDC = BN + 4;
   static constexpr size_t STAGE_BYTES = 3 * BU4 * 16;
-  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4;  // + EpLayerSeg's dst
+  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4;
   static constexpr size_t LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
 };
 
-#ifdef CGR_B3_STAMPS
-__device__ unsigned long long* b3_stamps;  // lab: [block][wave][4] s_memrealtime
-#define B3_STAMP(i)                                                                          \
-  if ((threadIdx.x & 63) == 0)                                                               \
-  {                                                                                          \
-    b3_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + (i)] =     \
-        __builtin_amdgcn_s_memrealtime();                                                    \
-    b3_stamps[((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 8 + 4 + (i)] = \
-        __builtin_amdgcn_s_memtime();                                                        \
-  }
-#else
-#define B3_STAMP(i)
-#endif
-#ifndef CGR_B3_LDA
-#define CGR_B3_LDA 4  // B fragment groups read from LDS ahead of the MFMAs that use them
-#endif
-#ifndef CGR_B3_LAB
-#define CGR_B3_LAB 0  // lab ablations (bit mask): 1 no loop loads, 2 no loop barrier, 4 no LDS B reads, 8 no staging
-#endif
+constexpr int B3_LDA = 4;  // B fragment groups read from LDS ahead of the MFMAs that use them
 
 // Pipeline (one barrier per k step, 3 LDS buffers for B):
 //   iteration ks computes step ks from LDS buffer ks % 3 and A fragments afr[ks & 1], and stages
@@ -219,40 +201,10 @@ __device__ unsigned long long* b3_stamps;  // lab: [block][wave][4] s_memrealtim
 //   Column groups are processed in pairs (CGR_B3_JPAIR): the six-term chains of two groups
 //   alternate, two independent accumulators in flight.
 //   Staging past the end writes a buffer nobody reads any more (unconditional, branch-free).
-// Optional by-product of an NT GEMM: its A operand as two row-major bf16 planes (hi, lo: the
-// split's first two pieces, exactly what the weight-gradient TN of gemm_b3tp.hpp multiplies), for
-// rows [0, round_up(M, 32)) (rows >= M written as zeros) and the k steps' columns.  Column tile tn
-// writes the k steps ks with ks % tiles_n == tn (each A element is loaded by every column tile).
-struct B3NoPlanes {
-  static constexpr bool on = false;
-  static constexpr bool copy = false;
-  uint16_t* hi;
-  uint16_t* lo;
-  int64_t ld;
-};
-struct B3PlaneOut {
-  static constexpr bool on = true;
-  static constexpr bool copy = false;
-  uint16_t* hi;
-  uint16_t* lo;
-  int64_t ld;  // >= nk * 32
-};
-// Other by-product: the A operand itself as fp32 rows of `cols` floats (ld, 16-byte aligned rows),
-// the masked values the split reads (zeros at k >= K): the x-GEMM reads x as it comes (8-byte rows)
-// and leaves the 16-byte-row copy the weight-gradient GEMMs read, instead of a padding pass ahead
-// of it.  Column tile tn writes the k steps ks with ks % tiles_n == tn.
-struct B3RowCopy {
-  static constexpr bool on = false;
-  static constexpr bool copy = true;
-  float* dst;
-  int64_t ld;
-  int cols;  // multiple of 4
-};
-
-template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP, class PO = B3NoPlanes>
+template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP>
 __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u4* __restrict__ Bimg,
                                                                int nimg, EP ep, int M, int N,
-                                                               int K, int tiles_n, PO po) {
+                                                               int K, int tiles_n) {
   using S = B3NtShape<WAVES, RF, NF>;
   constexpr int NT = S::NT, BM = S::BM, BN = S::BN, BU4 = S::BU4, BPT = S::BPT;
   extern __shared__ b3_u4 b3_lds[];
@@ -262,7 +214,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + B3_BK - 1) / B3_BK;
   const int sw = fg ^ lds_swz(fr);  // lds_swz(16 j + fr) == lds_swz(fr)
-  B3_STAMP(0)
 
   // ---- A: RF row fragments per lane, two float4 fetches per fragment per k step ----
   typename AL::Row arow[RF];
@@ -271,7 +222,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   typedef typename AL::Raw ARaw[RF][2];
   // unconditional loads: k >= K reads in-bounds element 0 (the loaders clamp), never used
   auto fetchA = [&](ARaw& a, int ks) {
-    if ((CGR_B3_LAB & 1) && ks > 2) return;
     const int kb = ks * B3_BK + 4 * fg;
 #pragma unroll
     for (int i = 0; i < RF; ++i) {
@@ -293,28 +243,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       }
       const float f[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
       b3_split8<3>(f, af[i]);
-      if constexpr (PO::copy) {
-        const int row = m0 + (w * RF + i) * 16 + fr;
-        if (ks % tiles_n == tn && row < M) {
-          float* o = po.dst + (int64_t)row * po.ld + kb;
-          if (kb < po.cols) *reinterpret_cast<float4*>(o) = u;
-          if (kb + 16 < po.cols) *reinterpret_cast<float4*>(o + 16) = v;
-        }
-      }
-      if constexpr (PO::on) {
-        const int row = m0 + (w * RF + i) * 16 + fr;
-        if (ks % tiles_n == tn && row < ((M + 31) & ~31) && ks < nk) {
-          const bool live = row < M;
-          const uint32_t z = 0;
-          typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-          const int64_t o = (int64_t)row * po.ld + ks * B3_BK + 4 * fg;
-          const b3_u4 h = af[i][0], l = af[i][1];
-          *reinterpret_cast<u2*>(po.hi + o) = live ? u2{h.x, h.y} : u2{z, z};
-          *reinterpret_cast<u2*>(po.hi + o + 16) = live ? u2{h.z, h.w} : u2{z, z};
-          *reinterpret_cast<u2*>(po.lo + o) = live ? u2{l.x, l.y} : u2{z, z};
-          *reinterpret_cast<u2*>(po.lo + o + 16) = live ? u2{l.z, l.w} : u2{z, z};
-        }
-      }
     }
   };
   // ---- B: the tile's column block of one (ks, piece) plane is BN * 4 contiguous b3_u4 ----
@@ -329,7 +257,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   }
   typedef b3_u4 BRaw[BPT];
   auto fetchB = [&](BRaw& b, int ks) {  // steps past the end re-read the last plane (unused)
-    if ((CGR_B3_LAB & 1) && ks > 2) return;
     const b3_u4* src = Bimg + (size_t)(ks < nk ? ks : nk - 1) * 3 * nimg * 4;
 #pragma unroll
     for (int p = 0; p < BPT; ++p) b[p] = src[boff[p]];
@@ -349,7 +276,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int LDA = CGR_B3_LDA < NF ? CGR_B3_LDA : NF - 1;
+  constexpr int LDA = B3_LDA < NF ? B3_LDA : NF - 1;
   // One step: the MFMAs of step ks (LDS buffer cb, fragments afc), column groups in pairs, with
   // the step's other work spread over them (the vector-memory path and the matrix pipe overlap
   // only when loads are interleaved with the MFMAs; issued as one burst per step they stall every
@@ -366,7 +293,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     const int kba = ksa * B3_BK + 4 * fg;
     const b3_u4* bsrc = Bimg + (size_t)(ksb < nk ? ksb : nk - 1) * 3 * nimg * 4;
     auto load_slot = [&](int s) {
-      if ((CGR_B3_LAB & 1) && ksa > 2) return;
       if (s < NAS) {
         ya[s >> 1][s & 1] = al.fetch(arow[s >> 1], kba + 16 * (s & 1), K);
       } else {
@@ -379,7 +305,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       const int o = (j * 16 + fr) * 4 + sw;
 #pragma unroll
       for (int q = 0; q < 3; ++q)
-        bq[j % RING][q] = (CGR_B3_LAB & 4) ? afc[0][q] + (b3_u4)(j) : Bs[q * BN * 4 + o];
+        bq[j % RING][q] = Bs[q * BN * 4 + o];
     };
 #pragma unroll
     for (int j = 0; j < LDA; ++j) rd(j);
@@ -425,7 +351,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
           load_slot(s);
           nvm += s < NAS ? AV : 1;
         }
-      if (!(CGR_B3_LAB & 8)) {
+      {
         const int w0 = p * BPT / NP, w1 = (p + 1) * BPT / NP;
 #pragma unroll
         for (int q = 0; q < BPT; ++q)
@@ -444,7 +370,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       if (two) b3_sgb<0x008>(MQ); else b3_sgb<0x008>(MQ);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!(CGR_B3_LAB & 2)) __syncthreads();
+    __syncthreads();
   };
 
   {  // prologue: buffers 0, 1 <- B(0), B(1); afr0 <- A(0); raw set 0 <- A(1), B(2)
@@ -460,7 +386,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     storeB(b1, 1);
     splitA(a0, afr0, 0);
     __syncthreads();
-    B3_STAMP(1)
     int cb = 0;  // LDS buffer of step ks (ks % 3)
     for (int ks = 0; ks < nk; ks += 2) {
       // even step: consume set 0 (A(ks+1), B(ks+2)), fill set 1 with A(ks+2), B(ks+3)
@@ -473,7 +398,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     }
   }
 
-  B3_STAMP(2)
   // ---- epilogue (the stage buffers are dead after the last barrier) ----
   constexpr int C4 = BN / 4;
   constexpr int EIT = (BM * C4 + NT - 1) / NT;
@@ -486,14 +410,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     pv[it] = ep.pre4(m0 + r, n0 + 4 * c4);
   }
   float* C = reinterpret_cast<float*>(b3_lds);
-  constexpr bool SEG = std::is_same<EP, EpLayerSeg>::value;
-  int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG: dst of rows m0 - 1 .. m0 + BM
-  if constexpr (SEG) {
-    for (int q = tid; q < BM + 2; q += NT) {
-      const int r = m0 - 1 + q;
-      sd[q] = (r >= 0 && r < M) ? ep.dst_s[r] : -1 - (r >= M);  // distinct sentinels
-    }
-  }
 #pragma unroll
   for (int i = 0; i < RF; ++i)
 #pragma unroll
@@ -508,66 +424,27 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     if (q < BM * C4) {
       const int r = q / C4, c4 = q - r * C4;
       const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
-      if constexpr (SEG)
-        *reinterpret_cast<float4*>(&C[r * S::LDC + 4 * c4]) =
-            ep.apply4p_h(m0 + r, n0 + 4 * c4, v, pv[it], cx);
-      else
-        ep.apply4p(m0 + r, n0 + 4 * c4, v, pv[it], cx);
+      ep.apply4p(m0 + r, n0 + 4 * c4, v, pv[it], cx);
     }
   }
-  if constexpr (SEG) {
-    // segments wholly inside [m0, m0 + nrow): thread (chunk of 16 rows, float4 column) sums the
-    // segments that START in its chunk, running past the chunk's end as needed
-    __syncthreads();
-    const int nrow = min(BM, M - m0);
-    constexpr int NCH = BM / 16;
-    for (int q = tid; q < NCH * C4; q += NT) {
-      const int ch = q / C4, c4 = q - ch * C4;
-      const int col = n0 + 4 * c4;
-      if (col >= ep.N) continue;
-      int s = 16 * ch;
-      const int end = min(16 * ch + 16, nrow);
-      // skip the tail of a segment begun before this chunk (in this tile or the previous one)
-      while (s < end && sd[s + 1] == sd[s]) ++s;
-      while (s < end) {
-        const int v = sd[s + 1];
-        float4 a = f4zero();
-        int r = s;
-        for (; r < nrow && sd[r + 1] == v; ++r)
-          a = f4add(a, *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]));
-        if (r < nrow || sd[nrow + 1] != v)  // ended inside the tile (else: crosses, fixup)
-          *reinterpret_cast<float4*>(ep.aout + (int64_t)v * ep.lda + col) = a;
-        s = r;
-      }
-    }
-  }
-  B3_STAMP(3)
 }
 
-template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP, class PO = B3NoPlanes>
+template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP>
 inline hipError_t launch_b3nt_t(const AL& al, const b3_u4* Bimg, int nimg, const EP& ep, int M,
-                                int N, int K, int tiles_n, hipStream_t st, const PO& po = PO{}) {
+                                int N, int K, int tiles_n, hipStream_t st) {
   using S = B3NtShape<WAVES, RF, NF>;
-  auto kern = gemm_b3nt_kernel<WAVES, RF, NF, NOMASK, AL, EP, PO>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  auto kern = gemm_b3nt_kernel<WAVES, RF, NF, NOMASK, AL, EP>;
+  static LdsLimit lim;
+  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), 160 * 1024);
+  if (e != hipSuccess) return e;
   const int tm = (M + S::BM - 1) / S::BM;
   hipLaunchKernelGGL(kern, dim3(tm * tiles_n), dim3(WAVES * 64), S::LDS_BYTES, st, al, Bimg, nimg,
-                     ep, M, N, K, tiles_n, po);
+                     ep, M, N, K, tiles_n);
   return hipGetLastError();
 }
 
 // workgroup rows: 8 waves (128 rows) when that still gives ~200+ workgroups, else 4 (64 rows)
-#ifndef CGR_B3_WAVES
-#define CGR_B3_WAVES 0  // 0: by size; 4 / 8: forced (lab)
-#endif
 inline int b3nt_waves(int M, int N) {
-  if (CGR_B3_WAVES) return CGR_B3_WAVES;
   const int tiles_n = b3_cols(N).tiles;
   return ((M + 127) / 128) * tiles_n >= 192 ? 8 : 4;
 }
@@ -576,9 +453,9 @@ inline int b3nt_waves(int M, int N) {
 inline int b3nt_rows(int M, int N) { return b3nt_waves(M, N) == 8 ? 128 : 64; }
 
 // C = A B^T with B given as its image (b3_pack of the same N, K).  M, N, K > 0.
-template <class AL, class EP, class PO = B3NoPlanes>
+template <class AL, class EP>
 inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int M, int N, int K,
-                              hipStream_t st, const PO& po = PO{}) {
+                              hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
   const B3Cols c = b3_cols(N);
   const bool w8 = b3nt_waves(M, N) == 8;
@@ -586,15 +463,11 @@ inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int
   // finite in-bounds data, multiplied by the image's zero rows)
   auto go = [&](auto NFc) -> hipError_t {
     constexpr int NF = decltype(NFc)::value;
-#ifndef CGR_B3_RF
-#define CGR_B3_RF 1  // row fragments per wave of the 128-row tiles (2: 4 waves x 32 rows)
-#endif
-    constexpr int W8 = 8 / CGR_B3_RF;
     if (K % 4 == 0)
-      return w8 ? launch_b3nt_t<W8, CGR_B3_RF, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po)
-                : launch_b3nt_t<4, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po);
-    return w8 ? launch_b3nt_t<W8, CGR_B3_RF, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po)
-              : launch_b3nt_t<4, 1, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st, po);
+      return w8 ? launch_b3nt_t<8, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st)
+                : launch_b3nt_t<4, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
+    return w8 ? launch_b3nt_t<8, 1, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st)
+              : launch_b3nt_t<4, 1, NF, false>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
   };
   switch (c.nf) {
     case 1: return go(std::integral_constant<int, 1>{});
@@ -737,9 +610,6 @@ struct B3TnSrc<LdGatherDiff<X>> {  // a[src] - h[rev]: loads 0..7 the a rows, 8.
   static bool fits(const LdGatherDiff<X>& l, int R) { return (double)R * l.ld < 4.0e9; }
 };
 
-#ifndef CGR_B3TN_LAB
-#define CGR_B3TN_LAB 0  // lab ablations (tools/b3tn_lab): 1 no MFMA, 2 no loads, 4 no staging
-#endif
 template <int TNN, int TNK, class AL, class BL>
 __global__ __launch_bounds__((B3TnShape<TNN, TNK>::NT)) void gemm_b3tn_kernel(
     AL al, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout, int R,
@@ -799,11 +669,6 @@ __global__ __launch_bounds__((B3TnShape<TNN, TNK>::NT)) void gemm_b3tn_kernel(
     }
   };
   auto fetch = [&]() {
-    if constexpr ((CGR_B3TN_LAB & 2) != 0) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) raw[i] = make_float4(off[i] * 1e-9f, 0.f, 1.f, 2.f);
-      return;
-    }
 #pragma unroll
     for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const float4*>(base0 + off[i]);
     if constexpr (TB::NL == 16) {
@@ -824,10 +689,6 @@ __global__ __launch_bounds__((B3TnShape<TNN, TNK>::NT)) void gemm_b3tn_kernel(
   // A rows past the split are zeroed (their products vanish whatever B holds there); columns
   // past Nout / Kout land in discarded outputs
   auto stage = [&](int t, int buf) {
-    if constexpr ((CGR_B3TN_LAB & 4) != 0) {
-      if (raw[0].x == 123.f && raw[15].y == 7.f) b3_lds[tid] = b3_u4{1, 2, 3, 4};
-      return;
-    }
     const int e0 = e_begin + t * 32;
     b3_u4* img = b3_lds + buf * SU4;
     float4 u[8];
@@ -877,7 +738,6 @@ __global__ __launch_bounds__((B3TnShape<TNN, TNK>::NT)) void gemm_b3tn_kernel(
     return q < S::REM ? q : 0;
   };
   auto compute = [&](int buf) {
-    if constexpr ((CGR_B3TN_LAB & 1) != 0) return;
     const b3_u4* img = b3_lds + buf * SU4;
     b3_u4 ah[RN > 0 ? RN : 1], al2[RN > 0 ? RN : 1];
 #pragma unroll
@@ -971,27 +831,20 @@ inline hipError_t launch_b3tn_t(const AL& al, const BL& bl, const B3TnPlan& p, f
                                 hipStream_t st) {
   using S = B3TnShape<TNN, TNK>;
   auto kern = gemm_b3tn_kernel<TNN, TNK, AL, BL>;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static LdsLimit lim;
+  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), 160 * 1024);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(p.tiles_k * p.splits), dim3(S::NT), S::LDS_BYTES, st, al, bl, slab,
                      bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
   return hipGetLastError();
 }
 
-#ifndef CGR_B3TN_TNK
-#define CGR_B3TN_TNK 5  // k fragments per workgroup (H = 400: 25 -> 5 tiles exactly)
-#endif
-#ifndef CGR_B3TN_TARGET
-#define CGR_B3TN_TARGET 176  // workgroups (A/B in the step: 128 -0.8 %, 256 -1.1 % vs 176; the side
-                             // stream shares the GPU with the main chain, fewer splits = smaller slabs)
-#endif
-inline B3TnPlan b3tn_plan(int Nout, int Kout, int R, int target = CGR_B3TN_TARGET) {
-  return plan_b3tn(Nout, Kout, R, CGR_B3TN_TNK, target);
+constexpr int kB3TnTnk = 5;  // k fragments per workgroup (H = 400: 25 -> 5 tiles exactly)
+// workgroups of the layer weight gradient (A/B in the step: 128 -0.8 %, 256 -1.1 % vs 176; the
+// side stream shares the GPU with the main chain, fewer splits = smaller slabs)
+constexpr int kB3TnTarget = 176;
+inline B3TnPlan b3tn_plan(int Nout, int Kout, int R, int target = kB3TnTarget) {
+  return plan_b3tn(Nout, Kout, R, kB3TnTnk, target);
 }
 // the A side (Nout) is held whole per workgroup: supported n-fragment counts; operand extents
 // must fit the 32-bit element offsets
@@ -1008,7 +861,7 @@ template <class AL, class BL>
 inline hipError_t launch_b3tn(const AL& al, const BL& bl, const B3TnPlan& p, float* slab,
                               float* bslab, int Nout, int Kout, int R, bool want_bias,
                               hipStream_t st) {
-  constexpr int TNK = CGR_B3TN_TNK;
+  constexpr int TNK = kB3TnTnk;
   if (!b3tn_ok(al, bl, Nout, R)) return hipErrorInvalidValue;
   switch (p.tnn) {
     case 25: return launch_b3tn_t<25, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);

@@ -22,25 +22,9 @@
 namespace cgr {
 
 // F consecutive floats p[0 .. F-1] (4-byte aligned: gfx950 global loads need no 16-byte alignment)
-#ifndef CGR_TNR_LD
-#define CGR_TNR_LD 0  // lab: 0 = one 16-byte load (4-byte aligned) + scalars, 1 = scalars only,
-                      // 2 = two 16-byte-aligned 16-byte loads + shift (F <= 5)
-#endif
 template <int F>
 __device__ __forceinline__ void tnr_ld(const float* __restrict__ p, float (&v)[F]) {
-  if constexpr (CGR_TNR_LD == 1) {
-#pragma unroll
-    for (int i = 0; i < F; ++i) v[i] = p[i];
-  } else if constexpr (CGR_TNR_LD == 2 && F > 4) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const float4* q = reinterpret_cast<const float4*>(a & ~uintptr_t(15));
-    const int d = (int)((a >> 2) & 3);
-    const float4 u = q[0], w = q[1];
-    const float e[8] = {u.x, u.y, u.z, u.w, w.x, w.y, w.z, w.w};
-#pragma unroll
-    for (int i = 0; i < F; ++i)
-      v[i] = d == 0 ? e[i] : (d == 1 ? e[i + 1] : (d == 2 ? e[i + 2] : e[(i + 3) & 7]));
-  } else if constexpr (F >= 4) {
+  if constexpr (F >= 4) {
     float4 q;
     __builtin_memcpy(&q, p, 16);
     v[0] = q.x;
@@ -133,9 +117,8 @@ struct TnrPlan {
 };
 
 constexpr int TNR_WAVES = 4;
-#ifndef CGR_TNR_PF
-#define CGR_TNR_PF 2  // data loads 2 steps (8 rows) ahead of the MFMAs, row indices 3
-#endif
+// data loads 2 steps (8 rows) ahead of the MFMAs, row indices 3
+constexpr int kTnrPf = 2;
 
 template <int FA, int FB, class SA, class SB>
 __global__ __launch_bounds__(TNR_WAVES * 64, 2) void gemm_tnr_kernel(
@@ -182,7 +165,7 @@ __global__ __launch_bounds__(TNR_WAVES * 64, 2) void gemm_tnr_kernel(
   };
   // index rows (gathered sources) are loaded one step ahead of the data loads, which are one step
   // ahead of the MFMAs: no load waits on another load inside a step
-  constexpr int NB = CGR_TNR_PF + 1;  // register sets: data CGR_TNR_PF steps ahead
+  constexpr int NB = kTnrPf + 1;  // register sets: data kTnrPf steps ahead
   typename SA::template Raw<FA> ra[NB];
   typename SB::template Raw<FB> rb[NB];
   typename SA::Idx ia[NB];
@@ -217,44 +200,27 @@ __global__ __launch_bounds__(TNR_WAVES * 64, 2) void gemm_tnr_kernel(
     // steps past my_steps re-read a valid row (never consumed)
     auto cl = [&](int t) { return t < my_steps ? t : my_steps - 1; };
     int t = 0;
-    if constexpr (CGR_TNR_PF == 2) {
-      fetch_idx(0, 0);
-      fetch_idx(cl(1), 1);
-      fetch_idx(cl(2), 2);
+    fetch_idx(0, 0);
+    fetch_idx(cl(1), 1);
+    fetch_idx(cl(2), 2);
+    fetch(0);
+    fetch(1);
+    for (; t + 3 <= my_steps; t += 3) {
+      fetch(2);
+      fetch_idx(cl(t + 3), 0);
+      compute(0);
+      __builtin_amdgcn_sched_barrier(0);
       fetch(0);
+      fetch_idx(cl(t + 4), 1);
+      compute(1);
+      __builtin_amdgcn_sched_barrier(0);
       fetch(1);
-      for (; t + 3 <= my_steps; t += 3) {
-        fetch(2);
-        fetch_idx(cl(t + 3), 0);
-        compute(0);
-        __builtin_amdgcn_sched_barrier(0);
-        fetch(0);
-        fetch_idx(cl(t + 4), 1);
-        compute(1);
-        __builtin_amdgcn_sched_barrier(0);
-        fetch(1);
-        fetch_idx(cl(t + 5), 2);
-        compute(2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (t < my_steps) compute(0);
-      if (t + 1 < my_steps) compute(1);
-    } else {
-      fetch_idx(0, 0);
-      fetch_idx(cl(1), 1);
-      fetch(0);
-      for (; t + 2 <= my_steps; t += 2) {
-        fetch(1);  // data of step t + 1
-        fetch_idx(cl(t + 2), 0);
-        compute(0);  // step t
-        __builtin_amdgcn_sched_barrier(0);
-        fetch(0);  // data of step t + 2
-        fetch_idx(cl(t + 3), 1);
-        compute(1);  // step t + 1
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (t < my_steps) compute(0);
+      fetch_idx(cl(t + 5), 2);
+      compute(2);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    if (t < my_steps) compute(0);
+    if (t + 1 < my_steps) compute(1);
   }
 
   // ---- fixed-order combine of the 4 waves' partial tiles: (w0 + w1) + (w2 + w3) ----

@@ -45,34 +45,6 @@ __global__ __launch_bounds__(256) void k_segsum_v4(const float* __restrict__ val
   *reinterpret_cast<float4*>(out + v * ldo + 4 * c) = acc;
 }
 
-// segsum_fixup: thread (segment, float4 column); same row order as k_segsum_v4
-__global__ __launch_bounds__(256) void k_segsum_fixup(const float* __restrict__ vals, int64_t ldv,
-                                                      const int* __restrict__ ptr, int64_t nseg,
-                                                      int C4, int tile_rows,
-                                                      float* __restrict__ out, int64_t ldo) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nseg * C4) return;
-  const int64_t v = t / C4;
-  const int c = (int)(t - v * C4);
-  const int b = ptr[v], e = ptr[v + 1];
-  if (b < e && b / tile_rows == (e - 1) / tile_rows) return;  // written by its tile
-  float4 acc = f4zero();
-  for (int j = b; j < e; ++j)
-    acc = f4add(acc, *reinterpret_cast<const float4*>(vals + (int64_t)j * ldv + 4 * c));
-  *reinterpret_cast<float4*>(out + v * ldo + 4 * c) = acc;
-}
-
-hipError_t segsum_fixup(const float* vals, int64_t ldv, const int* ptr, int64_t nseg,
-                        int64_t width, int tile_rows, float* out, int64_t ldo, hipStream_t st) {
-  if (nseg <= 0 || width <= 0) return hipSuccess;
-  if (width % 4 || ldv % 4 || ldo % 4 || tile_rows <= 0) return hipErrorInvalidValue;
-  const int C4 = (int)(width / 4);
-  const int64_t tot = nseg * C4;
-  hipLaunchKernelGGL(k_segsum_fixup, dim3(cdiv(tot, 256)), dim3(256), 0, st, vals, ldv, ptr, nseg,
-                     C4, tile_rows, out, ldo);
-  return hipGetLastError();
-}
-
 template <bool GATHER>
 __global__ __launch_bounds__(256) void k_segsum_s(const float* __restrict__ vals, int64_t ldv,
                                                   const int* __restrict__ idx,
@@ -207,10 +179,7 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
 // all those edges (the per-edge kernel reloaded it for every edge: 14 float4 + 14 scalar loads
 // per output float4), and sums its edges' h0 into a_0 in edge order -- the same adds, in the same
 // order, as k_edge_init followed by k_segsum_v4<false>, so h0 / pre0 / a_0 are bitwise unchanged.
-#ifndef CGR_EI_NODES
-#define CGR_EI_NODES 4
-#endif
-constexpr int kEiNodes = CGR_EI_NODES;
+constexpr int kEiNodes = 4;
 constexpr int kEiMaxFe = 16;
 
 template <bool REG>
@@ -218,7 +187,7 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
     const float* __restrict__ P, const int* __restrict__ src_s, const float* __restrict__ e_s,
     int Fe, int Fep, const float* __restrict__ w0eT, const float* __restrict__ b0,
     const int* __restrict__ dst_ptr, int64_t N, int H, int Hp, int act, float* __restrict__ h0,
-    float* __restrict__ pre0, float* __restrict__ a, uint8_t* __restrict__ h0bits) {
+    float* __restrict__ pre0, float* __restrict__ a) {
   const int C4 = Hp >> 2;
   const int c = threadIdx.x;
   if (c >= C4) return;  // no barriers below
@@ -277,9 +246,6 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
       h.z = act_fwd(z.z, act);
       h.w = act_fwd(z.w, act);
       *reinterpret_cast<float4*>(h0 + o) = h;
-      if (CGR_HBITS && h0bits)
-        h0bits[(int64_t)i * C4 + c] = (uint8_t)((h.x > 0.f) | ((h.y > 0.f) << 1) |
-                                                ((h.z > 0.f) << 2) | ((h.w > 0.f) << 3));
       acc = f4add(acc, h);
     }
     *reinterpret_cast<float4*>(a + v * Hp + n) = acc;
@@ -289,17 +255,17 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
 hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
                                 int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
                                 int64_t N, int H, int Hp, int act, float* h0, float* pre0,
-                                float* a, hipStream_t st, uint8_t* h0bits) {
+                                float* a, hipStream_t st) {
   if (N <= 0) return hipSuccess;
   if (Hp % 4 || Hp / 4 > 128) return hipErrorInvalidValue;  // one thread per float4 column
   const int threads = (Hp / 4 + 63) / 64 * 64;
   const int nb = (int)cdiv(N, kEiNodes);
   if (Fe <= kEiMaxFe && (Fe == 0 || Fep % 4 == 0))
     hipLaunchKernelGGL(k_edge_init_seg<true>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
-                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a, h0bits);
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
   else
     hipLaunchKernelGGL(k_edge_init_seg<false>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
-                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a, h0bits);
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
   return hipGetLastError();
 }
 
@@ -407,66 +373,13 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
   return hipGetLastError();
 }
 
-// Head blocks of k_readout_bwd (blocks past the dzn ones): 64 columns x 4 row phases each;
-// dwf[n] = sum_b dy[b] g[b, n], dbf = sum_b dy[b], phases combined in fixed order.
-struct HeadBwd {
-  const float* g;
-  int64_t B;
-  float* dwf;
-  float* dbf;
-  int first_block;  // blocks below compute dzn
-};
-
-__device__ __forceinline__ void head_bwd_block(const float* __restrict__ dy, const HeadBwd& hb,
-                                               int blk, int H, int Hp) {
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  const int n = blk * 64 + tx;
-  float acc = 0.f, sdy = 0.f;
-  const int B = (int)hb.B;
-  const int nc = n < H ? n : H - 1;
-  int b = ty;
-  for (; b + 28 < B; b += 32) {  // 8 rows' loads in flight per thread (latency, not bandwidth)
-    float d[8], gv[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      d[j] = dy[b + 4 * j];
-      gv[j] = hb.g[(int64_t)(b + 4 * j) * Hp + nc];
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      acc += d[j] * gv[j];
-      sdy += d[j];
-    }
-  }
-  for (; b < B; b += 4) {
-    const float d = dy[b];
-    acc += d * hb.g[(int64_t)b * Hp + nc];
-    sdy += d;
-  }
-  __shared__ float red[2][4][64];
-  red[0][ty][tx] = acc;
-  red[1][ty][tx] = sdy;  // every tx of a row phase summed the same dy values
-  __syncthreads();
-  if (ty == 0 && n < H)
-    hb.dwf[n] = (red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]);
-  if (blk == 0 && threadIdx.x == 0)
-    hb.dbf[0] = (red[1][0][0] + red[1][1][0]) + (red[1][2][0] + red[1][3][0]);
-}
-
-template <bool HEAD>
 __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dy,
                                                      const float* __restrict__ wf,
                                                      const int* __restrict__ node_graph,
                                                      const float* __restrict__ hn,
                                                      const float* __restrict__ zn, int64_t N,
                                                      int H, int Hp, int act,
-                                                     float* __restrict__ dzn, HeadBwd hb) {
-  if constexpr (HEAD) {
-    if ((int)blockIdx.x >= hb.first_block) {
-      head_bwd_block(dy, hb, (int)blockIdx.x - hb.first_block, H, Hp);
-      return;
-    }
-  }
+                                                     float* __restrict__ dzn) {
   const int C4 = Hp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * C4) return;
@@ -499,25 +412,10 @@ __global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ d
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
                            float* dzn, hipStream_t st) {
-  return head_readout_bwd(dy, nullptr, 0, nullptr, nullptr, wf, node_graph, hn, zn, N, H, Hp, act,
-                          dzn, st);
-}
-
-hipError_t head_readout_bwd(const float* dy, const float* g, int64_t B, float* dwf, float* dbf,
-                            const float* wf, const int* node_graph, const float* hn,
-                            const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
-                            hipStream_t st) {
   const int64_t tot = N > 0 ? N * (Hp / 4) : 0;
-  const int rb = (int)cdiv(tot, 256);
-  const int hbk = dwf ? (int)cdiv(H, 64) : 0;
-  if (rb + hbk <= 0) return hipSuccess;
-  const HeadBwd hb{g, B, dwf, dbf, rb};
-  if (hbk)
-    hipLaunchKernelGGL(k_readout_bwd<true>, dim3(rb + hbk), dim3(256), 0, st, dy, wf, node_graph,
-                       hn, zn, N, H, Hp, act, dzn, hb);
-  else
-    hipLaunchKernelGGL(k_readout_bwd<false>, dim3(rb), dim3(256), 0, st, dy, wf, node_graph, hn,
-                       zn, N, H, Hp, act, dzn, hb);
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_readout_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dy, wf, node_graph,
+                     hn, zn, N, H, Hp, act, dzn);
   return hipGetLastError();
 }
 
@@ -526,37 +424,6 @@ hipError_t head_readout_bwd(const float* dy, const float* g, int64_t B, float* d
 // ------------------------------------------------------------------------------------------
 int layer_act_bwd_blocks(int64_t E, int Hp) { return (int)cdiv(E * (Hp / 4), 256); }
 
-// 2 fp32 -> packed bf16x2 (RNE) and the values it represents (gemm_b3.hpp b3_cvt2)
-typedef __bf16 kb_bf16x2 __attribute__((ext_vector_type(2)));
-typedef float kb_f2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t kb_cvt2(float a, float b, float& fa, float& fb) {
-  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(kb_f2{a, b}, kb_bf16x2));
-  fa = __uint_as_float(u << 16);
-  fb = __uint_as_float(u & 0xffff0000u);
-  return u;
-}
-// hi = bf16(x), lo = bf16(x - hi) of 4 values -> 8 bytes each at hi_p / lo_p
-__device__ __forceinline__ void kb_planes4(const float (&d)[4], uint16_t* hi_p, uint16_t* lo_p) {
-  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-  float f0, f1, f2, f3, g0, g1, g2, g3;
-  const uint32_t h01 = kb_cvt2(d[0], d[1], f0, f1), h23 = kb_cvt2(d[2], d[3], f2, f3);
-  const uint32_t l01 = kb_cvt2(d[0] - f0, d[1] - f1, g0, g1), l23 = kb_cvt2(d[2] - f2, d[3] - f3, g2, g3);
-  *reinterpret_cast<u2*>(hi_p) = u2{h01, h23};
-  *reinterpret_cast<u2*>(lo_p) = u2{l01, l23};
-}
-
-// ReLU mask of a float4 (bits of FloatView::hb when given, else the sign of h): as float4 of
-// 1 / 0 in m so the consumers test m.k > 0 either way
-__device__ __forceinline__ float4 relu_mask4(const uint8_t* bits, const float* h, int64_t i,
-                                             int n, int Hp) {
-  if (CGR_HBITS && bits) {  // (compiled out when off: one load form in the hot kernels)
-    const uint32_t b = bits[i * (Hp >> 2) + (n >> 2)];
-    return make_float4((float)(b & 1), (float)((b >> 1) & 1), (float)((b >> 2) & 1),
-                       (float)((b >> 3) & 1));
-  }
-  return *reinterpret_cast<const float4*>(h + i * Hp + n);
-}
-
 // one float4 of one edge row of the layer backward, given dh = dL/dh_{l+1}[i, n..n+3]:
 // dpre = dh * keep/(1-p) * act'(pre) ; dh0 (+)= sigma * dpre ; dsig += dpre . h0
 __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
@@ -564,7 +431,7 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
   const int64_t o = i * a.Hp + n;
   float d[4] = {dh.x, dh.y, dh.z, dh.w};
   if (a.act == ACT_RELU) {  // h_{l+1} > 0 <=> relu active and kept by dropout
-    const float4 hv = relu_mask4(a.hbits, a.hnext, i, n, a.Hp);
+    const float4 hv = *reinterpret_cast<const float4*>(a.hnext + o);
     const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
@@ -582,11 +449,7 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
   }
   const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
   *reinterpret_cast<float4*>(a.dpre + o) = dp;
-  if (a.dphi) {
-    const int64_t po = i * a.dpld + n;
-    kb_planes4(d, a.dphi + po, a.dplo + po);
-  }
-  if (a.dh0) {
+  {
     const float sg = a.sigma ? a.sigma[0] : 1.f;
     float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
     acc.x += sg * dp.x;
@@ -609,20 +472,7 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
 __device__ __forceinline__ void edge_init_bwd_row(const LayerBwdArgs& a, int64_t i, int n,
                                                   float4 dh) {
   const int64_t o = i * a.Hp + n;
-  float4 s0;
-  if (a.dh0) {
-    s0 = *reinterpret_cast<const float4*>(a.dh0 + o);
-  } else {  // deferred skip gradient: the layers' dpre, in the layer loop's order
-    s0 = f4zero();
-    for (int l = a.nl - 1; l >= 0; --l) {
-      const float4 dp = *reinterpret_cast<const float4*>(a.dpre_l[l] + o);
-      const float sg = a.sigma_l[l] ? a.sigma_l[l][0] : 1.f;
-      s0.x += sg * dp.x;
-      s0.y += sg * dp.y;
-      s0.z += sg * dp.z;
-      s0.w += sg * dp.w;
-    }
-  }
+  const float4 s0 = *reinterpret_cast<const float4*>(a.dh0 + o);
   float4 d = f4add(s0, dh);
   if (a.act == ACT_RELU) {
     const float4 h = *reinterpret_cast<const float4*>(a.h0 + o);
@@ -682,9 +532,8 @@ struct RowOps {
 __device__ __forceinline__ RowOps layer_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
   const int64_t o = i * a.Hp + n;
   RowOps r;
-  r.m = a.act == ACT_RELU ? relu_mask4(a.hbits, a.hnext, i, n, a.Hp)
-                          : *reinterpret_cast<const float4*>(a.pre + o);
-  r.acc = (a.dh0 && !a.first) ? *reinterpret_cast<const float4*>(a.dh0 + o) : f4zero();
+  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.hnext : a.pre) + o);
+  r.acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
   r.h0 = a.dsig_part ? *reinterpret_cast<const float4*>(a.h0 + o) : f4zero();
   return r;
 }
@@ -710,11 +559,7 @@ __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i
   }
   const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
   *reinterpret_cast<float4*>(a.dpre + o) = dp;
-  if (a.dphi) {
-    const int64_t po = i * a.dpld + n;
-    kb_planes4(d, a.dphi + po, a.dplo + po);
-  }
-  if (a.dh0) {
+  {
     const float sg = a.sigma ? a.sigma[0] : 1.f;
     float4 acc = r.acc;
     acc.x += sg * dp.x;
@@ -734,9 +579,8 @@ __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i
 __device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
   const int64_t o = i * a.Hp + n;
   RowOps r;
-  r.m = a.act == ACT_RELU ? relu_mask4(a.hbits, a.h0, i, n, a.Hp)
-                          : *reinterpret_cast<const float4*>(a.pre + o);
-  r.acc = a.dh0 ? *reinterpret_cast<const float4*>(a.dh0 + o) : f4zero();
+  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.h0 : a.pre) + o);
+  r.acc = *reinterpret_cast<const float4*>(a.dh0 + o);
   r.h0 = f4zero();
   return r;
 }
@@ -744,18 +588,7 @@ __device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t 
 __device__ __forceinline__ void edge_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
                                                const RowOps& r) {
   const int64_t o = i * a.Hp + n;
-  float4 s0 = r.acc;
-  if (!a.dh0) {  // deferred skip gradient: the layers' dpre, in the layer loop's order
-    for (int l = a.nl - 1; l >= 0; --l) {
-      const float4 dp = *reinterpret_cast<const float4*>(a.dpre_l[l] + o);
-      const float sg = a.sigma_l[l] ? a.sigma_l[l][0] : 1.f;
-      s0.x += sg * dp.x;
-      s0.y += sg * dp.y;
-      s0.z += sg * dp.z;
-      s0.w += sg * dp.w;
-    }
-  }
-  float4 d = f4add(s0, dh);
+  float4 d = f4add(r.acc, dh);
   if (a.act == ACT_RELU) {
     d.x = r.m.x > 0.f ? d.x : 0.f;
     d.y = r.m.y > 0.f ? d.y : 0.f;
@@ -925,9 +758,7 @@ hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStr
 // ~40k outputs still give >1000 workgroups.  The bias slabs [splits][Nout] ride along as extra
 // float4-less columns in the last workgroups.
 constexpr int kRedCols = 32, kRedGroups = 8;
-#ifndef CGR_REDUCE_MAX_BLOCKS
-#define CGR_REDUCE_MAX_BLOCKS 256  // A/B: 256 beats 64 and unbounded (4096) by 4-8 %
-#endif
+constexpr int kReduceMaxBlocks = 256;  // grouped form grid (A/B: beats 64 and unbounded 4096 by 4-8 %)
 
 // one logical block of one reduction job
 __device__ __forceinline__ void reduce_slab_block(const RedJob& J, int blk, float4 (*part)[kRedCols],
@@ -1083,20 +914,16 @@ __global__ __launch_bounds__(256) void k_reduce_slabs_flat(RedJob J) {
   }
 }
 
-#ifndef CGR_REDUCE_FLAT
-#define CGR_REDUCE_FLAT 0  // one thread per output, all splits in flight: serial 106 -> 97 us/step, but the step +3.5 % (A/B)
-#endif
-
-#ifndef CGR_REDUCE_FLAT_MAX_SPLITS
-#define CGR_REDUCE_FLAT_MAX_SPLITS 8  // flat form for short split counts (the grouped form leaves
-                                      // 8 - splits thread groups idle and iterates per block)
-#endif
+// flat form (one thread per output, every split in flight) for short split counts: the grouped
+// form leaves 8 - splits thread groups idle.  For every side-stream reduction the flat form was
+// serially faster (106 -> 97 us / step) but the step 3.5 % slower (A/B): it crowds the main chain.
+constexpr int kReduceFlatMaxSplits = 8;
 
 hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int Nout, int Kout,
                         float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                         hipStream_t st, int gap_at, int gap_len, bool flat) {
   RedJobs jobs{};
-  if (flat || CGR_REDUCE_FLAT || splits <= CGR_REDUCE_FLAT_MAX_SPLITS) {
+  if (flat || splits <= kReduceFlatMaxSplits) {
     if (!add_reduce_job(jobs, slab, bslab, splits, Nout, Kout, dst, ld_dst, col_off, bias_dst,
                         gap_at, gap_len) || jobs.n == 0)
       return hipSuccess;
@@ -1108,7 +935,7 @@ hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int N
   }
   add_reduce_job(jobs, slab, bslab, splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, gap_at,
                  gap_len);
-  return reduce_slabs_batched(jobs, CGR_REDUCE_MAX_BLOCKS, st);
+  return reduce_slabs_batched(jobs, kReduceMaxBlocks, st);
 }
 
 __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict__ part, int nb,

@@ -9,10 +9,6 @@ namespace cgr {
 // out[s, :w] = sum_{j in [ptr[s], ptr[s+1])} vals[idx ? idx[j] : j, :w]
 hipError_t segment_sum(const float* vals, int64_t ldv, const int* idx, const int* ptr,
                        int64_t nseg, int64_t width, float* out, int64_t ldo, hipStream_t st);
-// the segments segment_sum would write that a row-tiled producer (EpLayerSeg, tiles of
-// tile_rows rows from row 0) left out: empty ones and those crossing a tile boundary
-hipError_t segsum_fixup(const float* vals, int64_t ldv, const int* ptr, int64_t nseg,
-                        int64_t width, int tile_rows, float* out, int64_t ldo, hipStream_t st);
 
 struct TransposeJob {
   const float* src;  // [rows, ld_src], columns [col_off, col_off + cols)
@@ -34,7 +30,7 @@ hipError_t transpose_batch(const TransposeJobs& jobs, hipStream_t st);
 hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
                                 int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
                                 int64_t N, int H, int Hp, int act, float* h0, float* pre0,
-                                float* a, hipStream_t st, uint8_t* h0bits = nullptr);
+                                float* a, hipStream_t st);
 hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int Fe, int Fep,
                          const float* w0eT, const float* b0, int64_t E, int H, int Hp, int act,
                          float* h0, float* pre0, hipStream_t st);
@@ -48,12 +44,6 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
                     float* dg, float* dwf, float* dbf, hipStream_t st);
 
 // dzn[v] = dy[graph(v)] * wf * act'(zn[v])   (ReLU: hn > 0)
-// k_head_bwd's dwf / dbf column sums and readout_act_bwd's dzn in one launch (head blocks after
-// the dzn blocks)
-hipError_t head_readout_bwd(const float* dy, const float* g, int64_t B, float* dwf, float* dbf,
-                            const float* wf, const int* node_graph, const float* hn,
-                            const float* zn, int64_t N, int H, int Hp, int act, float* dzn,
-                            hipStream_t st);
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
                            float* dzn, hipStream_t st);
@@ -66,7 +56,6 @@ struct LayerBwdArgs {
   const int* dst_s;
   const int* rev_s;
   const float* hnext;  // h_{l+1} (ReLU mask)
-  const uint8_t* hbits;  // its mask bits (FloatView::hb; edge init: h_0's), or nullptr
   const float* pre;    // pre_{l} (non-ReLU)
   const float* h0;
   const float* sigma;  // skip weight (nullptr -> 1)
@@ -79,17 +68,8 @@ struct LayerBwdArgs {
   int64_t E;
   int H, Hp;
   float* dpre;
-  float* dh0;         // written (first) or accumulated; nullptr: not accumulated (deferred)
+  float* dh0;         // written (first) or accumulated (sigma-weighted dpre of every layer)
   float* dsig_part;   // [gridDim] partial sums of dpre*h0 (nullable)
-  // edge init with deferred dh0: dh0 = sum_{l = nl-1 .. 0} sigma_l dpre_l, summed in the order
-  // the per-layer accumulation would have used (bitwise the same)
-  int nl;
-  const float* dpre_l[32];
-  const float* sigma_l[32];
-  // dpre also as bf16 hi / lo planes [.][dpld] (the weight-gradient GEMM's A operand), or null
-  uint16_t* dphi;
-  uint16_t* dplo;
-  int64_t dpld;
 };
 // nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
 hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);

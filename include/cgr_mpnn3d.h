@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CGR_ABI_VERSION 2
+#define CGR_ABI_VERSION 3
 #define CGR_MAX_DEPTH 32
 
 enum cgr_status {
@@ -119,9 +119,10 @@ int cgr_graph_prep(const cgr_gnn_config* cfg, const cgr_batch* batch, void* aren
  * uint64, may be NULL) is given, by its value, which the forward then increments on the device:
  * a captured graph replays with a fresh mask each time (the key is kept in the arena for the
  * backward).  Fills `arena` with what cgr_gnn_backward needs.  `y` device [B].
- * `training` is a bit set: CGR_TRAIN_DROPOUT = train-mode dropout (module.training);
- * CGR_TRAIN_FOR_BACKWARD = a backward will follow (the forward may then write operand forms only
- * the weight-gradient GEMMs read).  Pass the same value to cgr_gnn_backward. */
+ * `training` is a bit set (other bits are rejected): CGR_TRAIN_DROPOUT = train-mode dropout
+ * (module.training); CGR_TRAIN_FOR_BACKWARD = a backward will follow (the forward then also packs
+ * the backward GEMMs' weight images into the arena; cgr_gnn_backward refuses an arena whose
+ * forward did not set it).  Pass the same value to cgr_gnn_backward. */
 #define CGR_TRAIN_DROPOUT 1
 #define CGR_TRAIN_FOR_BACKWARD 2
 int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params,
@@ -132,11 +133,20 @@ int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params,
 /* Reverse mode of cgr_gnn_forward (what autograd runs for the reference: GNN.py:76-145 under
  * loss.backward(), trainer.py:142-143).  `dy` device [B] = dLoss/dy; writes every parameter
  * gradient into the table `grads` (same order and shapes as `params`, overwritten, not
- * accumulated).  `arena` must come from the matching forward call; `workspace` is scratch. */
+ * accumulated).  `arena` must come from the matching forward call; `workspace` is scratch.
+ *
+ * `bucket_events` (NULL, or CGR_GRAD_BUCKETS(depth) hipEvent_t handles passed as void*): event b
+ * is recorded on a stream of the backward as soon as every gradient of bucket b is final, so a
+ * data-parallel caller can start bucket b's all-reduce while the rest of the backward runs
+ * (trainer.py:138-144 has one device).  Buckets, in the order they become ready:
+ *   0            edge_to_node.{weight,bias}, ffn.{weight,bias}
+ *   1 + k        convs.(depth-1-k).lin.{weight,bias}            k = 0 .. depth-1
+ *   depth + 1    edge_init.{weight,bias}, skip_weights.* (end of the backward, caller's stream) */
+#define CGR_GRAD_BUCKETS(depth) ((depth) + 2)
 int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params,
                      const cgr_batch* batch, const float* dropout_p, uint64_t seed,
                      int32_t training, const void* arena, const float* dy, float* const* grads,
-                     void* workspace, void* stream);
+                     void* workspace, void* const* bucket_events, void* stream);
 
 /* Segmented sum, the sum-scatter primitive of the path (PyG propagate aggr="add", GNN.py:134;
  * global_add_pool, GNN.py:110) over a CSR: out[s, :] = sum_{j in [seg_ptr[s], seg_ptr[s+1])}

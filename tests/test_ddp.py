@@ -44,6 +44,36 @@ def test_shard_batch_is_a_valid_collated_batch():
     np.testing.assert_array_equal(np.concatenate([p.y for p in parts]), b.y)
 
 
+def test_grad_layout_buckets_cover_every_parameter_once():
+    from cgr_mpnn_3D._amd.functional import grad_layout
+
+    for D, skip in ((1, False), (4, False), (6, True)):
+        H, F, Fe = 8, 10, 3
+        shapes = [(H, F + Fe), (H,)]
+        for _ in range(D):
+            shapes += [(H, H), (H,)]
+        shapes += [(H, F + H), (H,), (1, H), (1,)]
+        shapes += [()] * (D if skip else 0)
+        offs, buckets, total = grad_layout(shapes, D)
+        assert len(buckets) == D + 2  # CGR_GRAD_BUCKETS(depth)
+        cover = np.zeros(total, np.int64)
+        for o, sh in zip(offs, shapes):
+            n = int(np.prod(sh)) if sh else 1
+            cover[o:o + n] += 1
+        assert cover.max() == 1  # disjoint
+        inb = np.zeros(total, np.int64)
+        for a, b in buckets:
+            assert a % 4 == 0 and a <= b <= total
+            inb[a:b] += 1
+        assert np.array_equal(inb, cover)  # buckets hold exactly the parameters
+        # readiness order: bucket 0 = edge_to_node + ffn, then layers D-1 .. 0, last edge_init
+        assert buckets[0][0] == offs[2 + 2 * D] == 0
+        for k in range(D):
+            l = D - 1 - k
+            assert buckets[1 + k] == (offs[2 + 2 * l], offs[3 + 2 * l] + H)
+        assert buckets[-1][0] == offs[0]
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -71,13 +101,21 @@ def _worker(rank, world, port, q):
         part = shard_batch(full, rank, world)
         _, _, g = on.loss_and_grads(sd, part.x, part.edge_index, part.edge_attr, part.batch,
                                     part.y, 2, "relu", False, num_graphs=part.num_graphs)
-        flat = torch.from_numpy(np.concatenate([np.ravel(g[k]) for k in keys]))
+        from cgr_mpnn_3D._amd.functional import grad_layout
+
+        # the native backward's flat buffer: bucket order, 16-byte aligned buckets
+        offs, buckets, total = grad_layout([sd[k].shape for k in keys], 2)
+        flat = torch.zeros(total, dtype=torch.float64)
+        for k, o in zip(keys, offs):
+            flat[o:o + g[k].size] = torch.from_numpy(np.ravel(g[k]))
         m = install_grad_allreduce(_Model())
-        m._grad_bucket_hook(flat)  # what the native backward calls with its flat bucket
+        m._grad_bucket_hook(flat, buckets, None)  # what the native backward calls (no events)
         if rank == 0:
             _, _, gf = on.loss_and_grads(sd, full.x, full.edge_index, full.edge_attr, full.batch,
                                          full.y, 2, "relu", False, num_graphs=full.num_graphs)
-            ref = np.concatenate([np.ravel(gf[k]) for k in keys])
+            ref = np.zeros(total)
+            for k, o in zip(keys, offs):
+                ref[o:o + gf[k].size] = np.ravel(gf[k])
             q.put(float(np.abs(flat.numpy() - ref).max() / np.abs(ref).max()))
     finally:
         dist.destroy_process_group()

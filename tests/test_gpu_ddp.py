@@ -1,0 +1,107 @@
+"""GPU: the data-parallel gradient exchange on the HIP path (cgr_mpnn_3D._amd.ddp).
+
+The native backward records one ready event per gradient bucket (include/cgr_mpnn3d.h,
+CGR_GRAD_BUCKETS) and GradAllReduce starts each bucket's collective on a communication stream as
+soon as its event fires.  What is checked here, on one GPU:
+  * a bucket op that doubles the bucket in place: every gradient comes out exactly 2x the
+    hook-free gradient, eagerly and inside a captured training step -- each event fired after its
+    bucket's last write (an early event would let a later write overwrite the doubled values) and
+    the buckets cover every parameter once;
+  * a world-1 RCCL process group (backend "nccl", created in this process): the real
+    all_reduce(SUM) of every bucket inside a captured step leaves the gradients bitwise equal to
+    the run without the hook.
+The multi-rank arithmetic (sum of shard gradients == whole-batch gradient) is covered by
+tests/test_gpu_parity.py::test_cfg2_eight_shard_gradients_sum_to_whole_batch and, over gloo,
+tests/test_ddp.py.  Reference: the single-device step of train.py:109-114 / trainer.py:138-144.
+"""
+
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+
+from cgr_mpnn_3D._amd.ddp import install_grad_allreduce, remove_grad_allreduce
+from cgr_mpnn_3D._amd.synth import make_batch
+from cgr_mpnn_3D.models.GNN import GNN
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(dev, D=3, H=128, skip=True):
+    torch.manual_seed(0)
+    b = make_batch(24, n_atoms=30, n_bonds=30, n_mace=32, seed=91)
+    m = GNN(b.x.shape[1], 14, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D,
+            use_learnable_skip=skip).to(dev).train()
+    return m, b.to_torch(dev)
+
+
+def _grads(m, data):
+    params = list(m.parameters())
+    pred = m(data)
+    loss = torch.nn.MSELoss(reduction="sum")(pred, data.y)
+    return [g.detach().clone() for g in torch.autograd.grad(loss, params)]
+
+
+def _captured(m, data):
+    params = list(m.parameters())
+
+    def step():
+        pred = m(data)
+        loss = torch.nn.MSELoss(reduction="sum")(pred, data.y)
+        return torch.autograd.grad(loss, params)
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        out = step()
+    g.replay()
+    torch.cuda.synchronize()
+    return [t.detach().clone() for t in out]
+
+
+def test_bucket_events_order_every_bucket_eager_and_captured(cuda_device):
+    m, data = _model(cuda_device)
+    ref = _grads(m, data)
+    install_grad_allreduce(m, op=lambda t: t.mul_(2.0))
+    try:
+        eager = _grads(m, data)
+        torch.cuda.synchronize()
+        for a, r in zip(eager, ref):
+            assert torch.equal(a, 2.0 * r)
+        cap = _captured(m, data)
+        for a, r in zip(cap, ref):
+            assert torch.equal(a, 2.0 * r)
+    finally:
+        remove_grad_allreduce(m)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_world1_rccl_allreduce_inside_captured_step_is_bitwise_identity(cuda_device):
+    m, data = _model(cuda_device, D=4, H=400, skip=False)
+    ref = _captured(m, data)
+    store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=cuda_device)
+    try:
+        install_grad_allreduce(m)
+        eager = _grads(m, data)
+        cap = _captured(m, data)
+        for a, c, r in zip(eager, cap, ref):
+            assert torch.equal(a, r)
+            assert torch.equal(c, r)
+    finally:
+        remove_grad_allreduce(m)
+        dist.destroy_process_group()
