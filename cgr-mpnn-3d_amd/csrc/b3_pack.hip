@@ -44,37 +44,6 @@ __global__ __launch_bounds__(256) void k_b3_pack(B3PackJobs jobs) {
               (int64_t)gridDim.x * blockDim.x);
 }
 
-// blocks [0, pad_blocks): one float4 of xp per thread (two 8-byte loads when F is even); blocks
-// past them: the image jobs, (block - pad_blocks) = job * gx + bx
-__global__ __launch_bounds__(256) void k_b3_pack_pad(B3PackJobs jobs, B3PadJob pd, int pad_blocks,
-                                                     int gx) {
-  if ((int)blockIdx.x < pad_blocks) {
-    const int c4n = pd.ldp >> 2;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= pd.N * c4n) return;
-    const int64_t r = t / c4n;
-    const int k = 4 * (int)(t - r * c4n);
-    const float* src = pd.x + r * pd.F;
-    float4 v;
-    if ((pd.F & 1) == 0) {
-      const float2 u = k < pd.F ? *reinterpret_cast<const float2*>(src + k) : make_float2(0.f, 0.f);
-      const float2 w =
-          k + 2 < pd.F ? *reinterpret_cast<const float2*>(src + k + 2) : make_float2(0.f, 0.f);
-      v = make_float4(u.x, u.y, w.x, w.y);
-    } else {
-      v.x = k < pd.F ? src[k] : 0.f;
-      v.y = k + 1 < pd.F ? src[k + 1] : 0.f;
-      v.z = k + 2 < pd.F ? src[k + 2] : 0.f;
-      v.w = k + 3 < pd.F ? src[k + 3] : 0.f;
-    }
-    *reinterpret_cast<float4*>(pd.xp + r * pd.ldp + k) = v;
-    return;
-  }
-  const int b = (int)blockIdx.x - pad_blocks;
-  const int j = b / gx, bx = b - j * gx;
-  b3_pack_job(jobs.job[j], (int64_t)bx * blockDim.x + threadIdx.x, (int64_t)gx * blockDim.x);
-}
-
 hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st) {
   if (jobs.n <= 0) return hipSuccess;
   if (jobs.n > kMaxB3PackJobs) return hipErrorInvalidValue;
@@ -89,24 +58,39 @@ hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st) {
   return hipGetLastError();
 }
 
-static int b3_pack_gx(const B3PackJobs& jobs) {
-  int64_t mx = 0;
-  for (int i = 0; i < jobs.n; ++i) {
-    const int64_t t = (int64_t)jobs.job[i].nk * jobs.job[i].rows * 4;
-    mx = t > mx ? t : mx;
+// e-image of X [R, C] (gemm_b3.hpp, B3EImg): thread = (32-row step s, column c, 8-row chunk q),
+// chunk fastest, so the four lanes of one column write its 64-byte slot of a plane whole and a
+// wave's stores cover 16 consecutive slots; its 8 loads (rows 32 s + 8 q + j, column c) run over
+// 16 consecutive columns of 4 rows per instruction.  Rows >= R and columns >= C are written as 0.
+__global__ __launch_bounds__(256) void k_b3_eimage(const float* __restrict__ x, int64_t ld,
+                                                   int64_t R, int C, int cimg, int64_t steps,
+                                                   b3_u4* __restrict__ img) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= steps * cimg * 4) return;
+  const int q = (int)(t & 3);
+  const int64_t u = t >> 2;
+  const int c = (int)(u % cimg);
+  const int64_t s = u / cimg;
+  const int64_t r0 = s * 32 + 8 * q;
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int64_t r = r0 + j;
+    f[j] = (r < R && c < C) ? x[r * ld + c] : 0.f;
   }
-  int gx = (int)((mx + 255) / 256);
-  return gx < 1 ? 1 : (gx > 256 ? 256 : gx);
+  b3_u4 pc[2];
+  b3_split8<2>(f, pc);
+  img[((s * 2 + 0) * cimg + c) * 4 + q] = pc[0];
+  img[((s * 2 + 1) * cimg + c) * 4 + q] = pc[1];
 }
 
-hipError_t b3_pack_pad(const B3PackJobs& jobs, const B3PadJob& pad, hipStream_t st) {
-  if (jobs.n > kMaxB3PackJobs) return hipErrorInvalidValue;
-  const int64_t tot = pad.N * (pad.ldp >> 2);
-  const int pb = (int)((tot + 255) / 256);
-  const int gx = b3_pack_gx(jobs);
-  const int nb = pb + gx * (jobs.n > 0 ? jobs.n : 0);
-  if (nb <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_b3_pack_pad, dim3(nb), dim3(256), 0, st, jobs, pad, pb, gx);
+hipError_t b3_eimage(const float* x, int64_t ld, int64_t R, int C, b3_u4* img, hipStream_t st) {
+  const int64_t steps = (R + 31) / 32;
+  const int cimg = b3_eimg_cols(C);
+  const int64_t tot = steps * cimg * 4;
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_b3_eimage, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, x, ld, R,
+                     C, cimg, steps, img);
   return hipGetLastError();
 }
 

@@ -148,15 +148,6 @@ struct B3PackJobs {
   int n;
 };
 hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st);
-// x rows padded to ldp floats (F % 4 != 0), the same launch as the image jobs: the padding pass
-// and the x-GEMM's image pack run side by side instead of back to back
-struct B3PadJob {
-  const float* x;
-  int64_t N;
-  int F, ldp;
-  float* xp;
-};
-hipError_t b3_pack_pad(const B3PackJobs& jobs, const B3PadJob& pad, hipStream_t st);
 // append a job, launching the batch when it is full
 inline hipError_t b3_pack_add(B3PackJobs& jobs, const B3PackJob& j, hipStream_t st) {
   if (jobs.n == kMaxB3PackJobs) {
@@ -872,6 +863,350 @@ inline hipError_t launch_b3tn(const AL& al, const BL& bl, const B3TnPlan& p, flo
     case 2: return launch_b3tn_t<2, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
   }
   return hipErrorInvalidValue;
+}
+
+
+// ------------------------------------------------------------------------------------------
+// TN with the n-side operand as a pre-split e-image (weight gradients dW = A^T B whose A is
+// shared by every k-tile: dpre, dzn, Gs)
+// ------------------------------------------------------------------------------------------
+// e-image of X [R rows, C cols] (R = the TN's reduction dimension): per 32-row step s and piece p
+// (0 = hi = bf16(x), 1 = lo = bf16(x - hi)) a plane of `cimg` columns x 64 bytes, column c
+// holding the pieces of rows 32 s .. 32 s + 31 in order; rows >= R and columns >= C are zero.
+// Written once per matrix by b3_eimage (b3_pack.hip).  An MFMA A fragment (16 columns x 32 rows)
+// is then one coalesced 1 KB global load per piece: lane (fr, fg) takes column fr, rows
+// 8 fg .. 8 fg + 7 -- no transposition and no split inside the GEMM, where gemm_b3tn_kernel
+// re-staged and re-split the whole A operand in each of its tiles_k workgroups (5 at H = 400:
+// 83 % of its staging VALU, PMC 7.6 VALU per MFMA).
+struct B3EImg {
+  const b3_u4* img;  // 16-byte units: ((s * 2 + p) * cimg + c) * 4 + chunk
+  int cimg;          // columns, a multiple of 16
+};
+inline int b3_eimg_cols(int C) { return (C + 15) / 16 * 16; }
+inline size_t b3_eimg_bytes(int64_t R, int C) {
+  return (size_t)((R + 31) / 32) * 2 * (size_t)b3_eimg_cols(C) * 64;
+}
+hipError_t b3_eimage(const float* x, int64_t ld, int64_t R, int C, b3_u4* img, hipStream_t st);
+
+// Workgroup = CW = 8 compute waves + SW staging waves (warp-specialised: a wave runs one role for
+// the whole kernel, so the registers of the two roles are not live together).
+//   * compute wave w: n-fragments w, w + CW, ... (RN of them, all TNK k-fragments each) plus RX
+//     of the remaining (TNN % CW) x TNK products, dealt round-robin; its A fragments come straight
+//     from the e-image, one step ahead of the MFMAs (two register sets, loop unrolled by 2).
+//   * staging waves: the k-side operand B (TNK x 16 columns of the tile), as gemm_b3tn_kernel
+//     stages it (4 columns x one 8-row chunk per job, split into hi / lo, transposed into LDS),
+//     its loads issued a whole interval before they are staged and the gather's index loads one
+//     more interval ahead; chunk c = rows 8 c .. 8 c + 7 of the step, the e-image's order.
+//   * one barrier per step: compute reads LDS buffer t & 1 while staging fills (t + 1) & 1.
+//   * splits start on 32-row boundaries, so a split's last step reads only its own rows or the
+//     image's zero rows: A is never masked; B rows past R read row 0 (finite, times zero A).
+//   * bias (column sums of A) from the pieces, hi + lo per element: n-fragment f is summed by
+//     the k-tile min(f / TNK, tiles_k - 1), inside the compute wave that loads f (the remainder
+//     fragments by the wave holding their k-fragment-0 product).
+template <int TNN, int TNK>
+struct B3TniShape {
+  static constexpr int CW = 8;
+  static constexpr int BC = TNK * 16;
+  static constexpr int JB = BC;  // staging jobs (4 columns x one 8-row chunk; one per column)
+  static constexpr int SW = (JB + 63) / 64;
+  static constexpr int NT = (CW + SW) * 64;
+  static constexpr int RN = TNN / CW;
+  static constexpr int REM = (TNN % CW) * TNK;
+  static constexpr int RX = (REM + CW - 1) / CW;
+  static constexpr int NA = RN + RX;        // A fragments a compute wave loads per step
+  static constexpr int SU4 = 2 * BC * 4;    // b3_u4 per LDS stage buffer
+  static constexpr size_t LDS_BYTES = (size_t)2 * SU4 * 16;
+};
+
+template <int TNN, int TNK, class BL>
+__global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
+    B3EImg ai, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout,
+    int R, int rows_per_split, int tiles_k, int want_bias) {
+  typedef B3TnSrc<BL> TB;
+  using S = B3TniShape<TNN, TNK>;
+  constexpr int CW = S::CW, RN = S::RN, RX = S::RX, NA = S::NA, BC = S::BC, SU4 = S::SU4;
+  constexpr int JB = S::JB;
+  extern __shared__ b3_u4 b3_lds[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = lin / tiles_k, tkk = lin - split * tiles_k;
+  const int k0 = tkk * TNK * 16;
+  const int e_begin = split * rows_per_split;  // a multiple of 32
+  const int e_end = min(R, e_begin + rows_per_split);
+  const int nt = e_end > e_begin ? (e_end - e_begin + 31) / 32 : 0;
+
+  if (w >= CW) {
+    // ================= staging waves: B of step t + 1 into LDS buffer (t + 1) & 1 =============
+    const int q = tid - CW * 64;
+    const bool act = q < JB;
+    const int jc = q & 3;                     // chunk: rows 8 jc .. 8 jc + 7 of a step
+    const int jcol = (act ? q >> 2 : 0) * 4;  // first of the job's 4 columns in the tile
+    const int gcol = k0 + jcol;
+    const float* base0 = TB::base(bl, 0, gcol);
+    const float* base1 = TB::base(bl, 1, gcol);
+    float4 raw[16];  // (NL = 8 operand kinds use the first 8)
+    uint32_t off[TB::NL];
+    int ix[8][2];
+    auto rowof = [&](int t, int j) {
+      const int e = e_begin + t * 32 + 8 * jc + j;
+      return e < R ? e : 0;
+    };
+    auto index = [&](int t) {  // the gather's index loads of step t
+#pragma unroll
+      for (int j = 0; j < 8; ++j) TB::idx(bl, rowof(t, j), ix[j]);
+    };
+    auto fetch = [&]() {  // addresses from the last index(), then the data loads
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int h = 0; h < TB::NL / 8; ++h) off[8 * h + j] = TB::off(bl, ix[j], h, gcol, Kout);
+#ifdef CGR_TNI_LAB
+      if (CGR_TNI_LAB & 1) {
+        for (int i = 0; i < 16; ++i) raw[i] = make_float4(off[i & (TB::NL - 1)] * 1e-9f, 1.f, 2.f, 3.f);
+        return;
+      }
+#endif
+#pragma unroll
+      for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const float4*>(base0 + off[i]);
+      if constexpr (TB::NL == 16) {
+#pragma unroll
+        for (int i = 8; i < 16; ++i) raw[i] = *reinterpret_cast<const float4*>(base1 + off[i]);
+      }
+    };
+    auto put = [&](b3_u4* img, int t, const float (&f)[8]) {
+      b3_u4 pc[2];
+      b3_split8<2>(f, pc);
+      const int row = b3tn_sigma(jcol + t);
+      const int slot = jc ^ lds_swz(row);
+      img[row * 4 + slot] = pc[0];
+      img[(BC + row) * 4 + slot] = pc[1];
+    };
+    auto stage = [&](int buf) {
+      b3_u4* img = b3_lds + buf * SU4;
+#ifdef CGR_TNI_LAB
+      if (CGR_TNI_LAB & 8) {
+        if (raw[0].x == 123.f) img[tid] = b3_u4{1, 2, 3, 4};
+        return;
+      }
+#endif
+      float4 u[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) u[j] = TB::get(raw, j);
+      if (act) {
+        const float f0[8] = {u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x};
+        const float f1[8] = {u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y};
+        const float f2[8] = {u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z};
+        const float f3[8] = {u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w};
+        put(img, 0, f0);
+        put(img, 1, f1);
+        put(img, 2, f2);
+        put(img, 3, f3);
+      }
+    };
+    if (nt > 0) {
+      index(0);
+      fetch();  // step 0
+      index(1);
+      stage(0);
+      fetch();  // step 1
+      index(2);
+      __syncthreads();
+      // interval t (compute on step t): stage step t + 1, whose loads were issued one interval
+      // ago, then issue step t + 2's (index loads a further interval ahead)
+      for (int t = 0; t < nt; ++t) {
+        if (t + 1 < nt) stage((t + 1) & 1);
+        fetch();  // step t + 2
+        index(t + 3);
+        __syncthreads();
+      }
+    }
+    return;
+  }
+
+  // ================= compute waves =================
+  const int rrow = b3tn_sigma(fr);  // fragment reads: storage row of column fr of a block
+  const int sw = fg ^ lds_swz(rrow);
+  // this wave's A fragments: f < RN: n-fragment w + f CW; f >= RN: remainder product xq(f - RN)
+  auto xq = [&](int x) {
+    const int qq = w + x * CW;
+    return qq < S::REM ? qq : 0;
+  };
+  auto frag_n = [&](int f) { return f < RN ? w + f * CW : RN * CW + xq(f - RN) / TNK; };
+  // bias ownership (k-tile of n-fragment f) and, for remainder products, k-fragment 0 only
+  bool own[NA];
+#pragma unroll
+  for (int f = 0; f < NA; ++f) {
+    const int n = frag_n(f);
+    const int tile = min(n / TNK, tiles_k - 1);
+    own[f] = want_bias && tile == tkk && n < TNN &&
+             (f < RN || (w + (f - RN) * CW < S::REM && xq(f - RN) % TNK == 0));
+  }
+  float bsum[NA];
+#pragma unroll
+  for (int f = 0; f < NA; ++f) bsum[f] = 0.f;
+  const int s0 = e_begin / 32;
+  auto aload = [&](int t, b3_u4 (&a)[NA][2]) {
+#ifdef CGR_TNI_LAB
+    if (CGR_TNI_LAB & 2) {
+      for (int f = 0; f < NA; ++f) a[f][0] = a[f][1] = b3_u4{(uint32_t)t, 1u, 2u, 3u};
+      return;
+    }
+#endif
+    const int s = s0 + (t < nt ? t : nt - 1);
+    const b3_u4* base = ai.img + (size_t)s * 2 * ai.cimg * 4;
+#pragma unroll
+    for (int f = 0; f < NA; ++f) {
+      const int c = min(frag_n(f) * 16 + fr, ai.cimg - 1);  // fragments past the image: discarded
+      a[f][0] = base[c * 4 + fg];
+      a[f][1] = base[(ai.cimg + c) * 4 + fg];
+    }
+  };
+  floatx4 acc[RN > 0 ? RN : 1][TNK], accx[RX > 0 ? RX : 1];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int j = 0; j < TNK; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int x = 0; x < RX; ++x) accx[x] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf, const b3_u4 (&a)[NA][2]) {
+    const b3_u4* img = b3_lds + buf * SU4;
+#ifdef CGR_TNI_LAB
+    if (CGR_TNI_LAB & 4) {
+      acc[0][0][0] += (float)img[sw].x + (float)a[0][0].x;
+      return;
+    }
+#endif
+#pragma unroll
+    for (int x = 0; x < RX; ++x) {
+      const int rb = (xq(x) % TNK) * 16 + rrow;
+      const b3_u4 xbh = img[rb * 4 + sw], xbl = img[(BC + rb) * 4 + sw];
+      floatx4 c = accx[x];
+      c = b3_mfma(a[RN + x][1], xbh, c);
+      c = b3_mfma(a[RN + x][0], xbl, c);
+      accx[x] = b3_mfma(a[RN + x][0], xbh, c);
+    }
+#pragma unroll
+    for (int j = 0; j < TNK; ++j) {
+      if constexpr (RN > 0) {
+        const int row = j * 16 + rrow;
+        const b3_u4 bh = img[row * 4 + sw], bl_ = img[(BC + row) * 4 + sw];
+#pragma unroll
+        for (int i = 0; i < RN; ++i) {
+          floatx4 c = acc[i][j];
+          c = b3_mfma(a[i][1], bh, c);
+          c = b3_mfma(a[i][0], bl_, c);
+          acc[i][j] = b3_mfma(a[i][0], bh, c);
+        }
+      }
+    }
+#pragma unroll
+    for (int f = 0; f < NA; ++f)
+      if (own[f]) {  // sum of hi + lo over the lane's 8 rows
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t h = a[f][0][k], l = a[f][1][k];
+          s += (__uint_as_float(h << 16) + __uint_as_float(l << 16)) +
+               (__uint_as_float(h & 0xffff0000u) + __uint_as_float(l & 0xffff0000u));
+        }
+        bsum[f] += s;
+      }
+  };
+  if (nt > 0) {
+    b3_u4 a0[NA][2], a1[NA][2];
+    aload(0, a0);
+    __syncthreads();  // B(0) staged
+    for (int t = 0; t < nt; t += 2) {
+      aload(t + 1, a1);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(0, a0);
+      __syncthreads();
+      if (t + 1 >= nt) break;
+      aload(t + 2, a0);
+      __builtin_amdgcn_sched_barrier(0);
+      compute(1, a1);
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: accumulators straight to the slab (rows n = 16 nf + 4 fg + r, columns
+  // k0 + 16 j + fr: 64 contiguous bytes per row and register) ----
+  const int ldk = (Kout + 3) & ~3;
+  float* out = slab + (int64_t)split * Nout * ldk;
+  auto store = [&](int nf, int kf, const floatx4& c) {
+    const int col = k0 + kf * 16 + fr;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = nf * 16 + fg * 4 + r;
+      if (row < Nout && col < Kout) out[(int64_t)row * ldk + col] = c[r];
+    }
+  };
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int j = 0; j < TNK; ++j) store(w + i * CW, j, acc[i][j]);
+#pragma unroll
+  for (int x = 0; x < RX; ++x) {
+    const int qq = w + x * CW;
+    if (qq < S::REM) store(RN * CW + qq / TNK, qq % TNK, accx[x]);
+  }
+  if (want_bias) {
+#pragma unroll
+    for (int f = 0; f < NA; ++f) {
+      float v = bsum[f];
+      v += __shfl_xor(v, 16, 64);  // (g0 + g1), (g2 + g3)
+      v += __shfl_xor(v, 32, 64);  // (g0 + g1) + (g2 + g3), the same in every group
+      const int n = frag_n(f) * 16 + fr;
+      if (own[f] && fg == 0 && n < Nout) bslab[(int64_t)split * Nout + n] = v;
+    }
+  }
+}
+
+// splits of the e-image TN: rows_per_split a multiple of 32 (plan_b3tn rounds it)
+template <int TNN, int TNK, class BL>
+inline hipError_t launch_b3tni_t(const B3EImg& ai, const BL& bl, const B3TnPlan& p, float* slab,
+                                 float* bslab, int Nout, int Kout, int R, bool want_bias,
+                                 hipStream_t st) {
+  using S = B3TniShape<TNN, TNK>;
+  auto kern = gemm_b3tni_kernel<TNN, TNK, BL>;
+  static LdsLimit lim;
+  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), 160 * 1024);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(kern, dim3(p.tiles_k * p.splits), dim3(S::NT), S::LDS_BYTES, st, ai, bl,
+                     slab, bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
+  return hipGetLastError();
+}
+
+// the e-image TN covers Nout up to 32 fragments (H <= 512) and B operands whose extents fit the
+// 32-bit element offsets; A = the e-image of an [R, >= Nout] matrix
+template <class BL>
+inline bool b3tni_ok(const BL& bl, int Nout, int R) {
+  const int t = (Nout + 15) / 16;
+  return t >= 1 && t <= 32 && B3TnSrc<BL>::fits(bl, R);
+}
+
+template <class BL>
+inline hipError_t launch_b3tni(const B3EImg& ai, const BL& bl, const B3TnPlan& p, float* slab,
+                               float* bslab, int Nout, int Kout, int R, bool want_bias,
+                               hipStream_t st) {
+  constexpr int TNK = kB3TnTnk;
+  if (!b3tni_ok(bl, Nout, R) || p.rows_per_split % 32) return hipErrorInvalidValue;
+  switch (p.tnn) {
+    case 25: return launch_b3tni_t<25, TNK>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+    case 32: return launch_b3tni_t<32, TNK>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+    default: break;
+  }
+  // other widths: the smallest instantiated fragment count that covers Nout (extra fragments
+  // read the image's zero columns and are not stored)
+  const int t = p.tnn;
+  B3TnPlan q = p;
+  if (t <= 2) { q.tnn = 2; return launch_b3tni_t<2, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
+  if (t <= 4) { q.tnn = 4; return launch_b3tni_t<4, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
+  if (t <= 8) { q.tnn = 8; return launch_b3tni_t<8, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
+  if (t <= 16) { q.tnn = 16; return launch_b3tni_t<16, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
+  if (t <= 25) { q.tnn = 25; return launch_b3tni_t<25, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
+  q.tnn = 32;
+  return launch_b3tni_t<32, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st);
 }
 
 }  // namespace cgr

@@ -55,6 +55,25 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
   return launch_gemm_tnr<FA, FB>(sa, sb, q, slab, bslab, Nout, Kout, R, want_bias, st);
 }
 
+// split-bf16 TN with the n-side operand A [R, Nout] as an e-image (gemm_b3.hpp): A is split
+// once by b3_eimage into `img`, then every k-tile of the GEMM reads it pre-split
+template <class BL>
+static hipError_t b3tni_gemm(const char* name, const float* A, int64_t lda, void* img,
+                             const BL& bl, int Nout, int Kout, int R, float* slab, float* bslab,
+                             bool want_bias, TnPlan* plan, hipStream_t st,
+                             int target = kB3TnTarget) {
+  {
+    ProfScope _p("eimage", st);
+    const hipError_t e = b3_eimage(A, lda, R, Nout, static_cast<b3_u4*>(img), st);
+    if (e != hipSuccess) return e;
+  }
+  const B3TnPlan q = b3tn_plan(Nout, Kout, R, target);
+  *plan = TnPlan{1, q.tiles_k, q.splits, q.rows_per_split};
+  ProfScope _p(name, st);
+  return launch_b3tni(B3EImg{static_cast<const b3_u4*>(img), b3_eimg_cols(Nout)}, bl, q, slab,
+                      bslab, Nout, Kout, R, want_bias, st);
+}
+
 // split-bf16 TN (gemm_b3.hpp); same slab layout as tn_gemm
 template <class AL, class BL>
 static hipError_t b3tn_gemm(const char* name, const AL& al, const BL& bl, int Nout, int Kout, int R,
@@ -95,6 +114,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   float* slab2 = reinterpret_cast<float*>(ws + WL.slab2);
   float* bslab2 = reinterpret_cast<float*>(ws + WL.bslab2);
   float* dsig_part = reinterpret_cast<float*>(ws + WL.dsig_part);
+  void* img_side = ws + WL.img_side;
+  void* img_main = ws + WL.img_main;
 
   const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
 
@@ -121,9 +142,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       const int Fp = d.Fp;
       LdPlain<4> al{dzn, Hp};
       LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
-      if (b3tn_ok(al, bl, H, N) && ((uintptr_t)fv.xp & 15) == 0) {
-        HIP_RET(b3tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, slab, bslab, true, &p,
-                          side, kB3TnReadoutTarget));
+      if (b3tni_ok(bl, H, N) && ((uintptr_t)fv.xp & 15) == 0) {
+        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl, H, Fp + H, N, slab,
+                           bslab, true, &p, side, kB3TnReadoutTarget));
       } else if (tnr_x_ok(H, Fp + H, Fp, fv.xp)) {
         HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
                                 TnrConcat{fv.xp, Fp, fv.a[D], Hp, Fp}, H, Fp + H, N, slab, bslab,
@@ -135,11 +156,10 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       HIP_RET(tn_reduce(p, slab, bslab, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
                         grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F));
     } else {
-      const LdPlain<4> al4{dzn, Hp};
       const LdConcat<4> bl4{b->x, F, fv.a[D], Hp, F};
-      if (F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 && b3tn_ok(al4, bl4, H, N)) {
-        HIP_RET(b3tn_gemm("gemm_tn_wgrad_readout", al4, bl4, H, F + H, N, slab, bslab, true, &p,
-                          side, kB3TnReadoutTarget));
+      if (F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 && b3tni_ok(bl4, H, N)) {
+        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl4, H, F + H, N, slab,
+                           bslab, true, &p, side, kB3TnReadoutTarget));
       } else if (F % 4 == 0 && tnr_x_ok(H, F + H, F, b->x)) {
         HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
                                 TnrConcat{b->x, F, fv.a[D], Hp, F}, H, F + H, N, slab, bslab,
@@ -220,8 +240,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdGatherDiff<false> bl{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
       TnPlan p;
       const int tf = tnr_layer_frags(H);
-      if (b3tn_ok(al, bl, H, E)) {
-        HIP_RET(b3tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, slab, bslab, true, &p, side));
+      if (b3tni_ok(bl, H, E)) {
+        HIP_RET(b3tni_gemm("gemm_tn_wgrad_layer", dp, Hp, img_side, bl, H, H, E, slab, bslab,
+                           true, &p, side));
       } else if (tf == 5) {
         HIP_RET((tnr_gemm<5, 5>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},
                                 TnrDiff{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp}, H, H, E, slab,
@@ -292,10 +313,10 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     const int64_t ldx = fv.xp ? d.Fp : F;
     TnPlan p;
     const int Fx = fv.xp ? d.Fp : F;  // x columns the GEMM covers (pad columns are zero)
-    const LdPlain<4> gal{Gs, Hp}, gbl{xb, ldx};
-    if (ldx % 4 == 0 && ((uintptr_t)xb & 15) == 0 && b3tn_ok(gal, gbl, H, N)) {
-      HIP_RET(b3tn_gemm("gemm_tn_wgrad_node", gal, gbl, H, Fx, N, slab2, bslab2, Fe == 0, &p, st,
-                        kB3TnNodeTarget));
+    const LdPlain<4> gbl{xb, ldx};
+    if (ldx % 4 == 0 && ((uintptr_t)xb & 15) == 0 && b3tni_ok(gbl, H, N)) {
+      HIP_RET(b3tni_gemm("gemm_tn_wgrad_node", Gs, Hp, img_main, gbl, H, Fx, N, slab2, bslab2,
+                         Fe == 0, &p, st, kB3TnNodeTarget));
       // the flat reduce: this one ends the backward's main chain
       HIP_RET(tn_reduce(p, slab2, bslab2, H, Fx, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st, F,
                         Fx - F, true));
