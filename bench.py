@@ -94,6 +94,9 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("segsum_dst_fwd", D + 1, E * H, seg_dst)
     add("gemm_nt_layer_fwd", D, 2.0 * E * H * H,
         f4 * (N * H + E * H + E * H + H * H + H + E * H * (1 + pre)) + 2 * i4 * E)
+    # the same GEMM with a_{l+1} = segsum_dst(h_{l+1}) summed in its epilogue (EpLayerSeg)
+    add("gemm_nt_layer_seg_fwd", D, 2.0 * E * H * H + E * H,
+        f4 * (N * H + E * H + E * H + H * H + H + E * H * (1 + pre) + N * H) + 3 * i4 * E)
     add("gemm_nt_readout_fwd", 1, 2.0 * N * H * H, f4 * (N * H + N * H + H * H + H + 2 * N * H))
     add("pool_head_fwd", 1, 2.0 * N * H, f4 * (N * H + B * H + H + B) + i4 * (B + 1))
     # backward

@@ -7,6 +7,7 @@ namespace cgr {
 
 // C[r, c] = acc (+ bias[c])
 struct EpStore {
+  static constexpr bool kSeg = false;
   float* C;
   int64_t ld;
   int M, N;
@@ -58,6 +59,7 @@ struct EpStore {
 // D-MPNN layer (GNN.py:91-102):
 //   pre = (m W^T + b) + sigma * h0 ; h = dropout(act(pre))
 struct EpLayer {
+  static constexpr bool kSeg = false;
   const float* bias;
   const float* sigma;  // learnable skip weight (device scalar) or nullptr (= 1, GNN.py:97)
   const float* h0;
@@ -117,9 +119,45 @@ struct EpLayer {
   }
 };
 
+// EpLayer whose GEMM also produces the layer's scatter-add a[v] = sum_{dst(e) = v} h'[e]
+// (GNN.py:134) from its row tile (rows are dst-sorted; gemm_b3nt_kernel's SEG epilogue): the
+// "gather -> MLP -> segmented reduce" pass in one launch
+struct EpLayerSeg : EpLayer {
+  static constexpr bool kSeg = true;
+  const int* dst_s;  // [M] node of each (dst-sorted) row
+  float* aout;       // [nodes, lda]; crossing / empty segments zeroed beforehand
+  int64_t lda;
+  // apply4p that also returns the stored h (rows / columns outside: v unchanged)
+  __device__ __forceinline__ float4 apply4p_h(int r, int c, float4 v, const Pre& p,
+                                              const Ctx& cx) const {
+    if (r >= M || c >= N) return v;
+    const int64_t o = (int64_t)r * ld + c;
+    float z[4] = {v.x, v.y, v.z, v.w};
+    const float h0v[4] = {p.h0.x, p.h0.y, p.h0.z, p.h0.w};
+    const float bv[4] = {p.b.x, p.b.y, p.b.z, p.b.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) z[k] = (z[k] + bv[k]) + cx.sg * h0v[k];
+    if (pre) *reinterpret_cast<float4*>(pre + o) = make_float4(z[0], z[1], z[2], z[3]);
+    float h[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      h[k] = act_fwd(z[k], act);
+      if (thresh)
+        h[k] = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
+                                                                                    : 0.f;
+      else
+        h[k] *= scale;
+    }
+    const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<float4*>(hout + o) = hv;
+    return hv;
+  }
+};
+
 // merged x-GEMM output [N, 2H]: columns [0, H) -> P (edge-init half), [H, 2H) -> Q (readout's
 // x-part); both internal [N, ld] buffers.
 struct EpSplit2 {
+  static constexpr bool kSeg = false;
   float* P;
   float* Q;
   int64_t ld;
@@ -151,6 +189,7 @@ struct EpSplit2 {
 
 // readout with the x-part precomputed: hn = act((s W_n[:, F:]^T + Q) + b_n)   (GNN.py:106-107)
 struct EpReadoutQ {
+  static constexpr bool kSeg = false;
   const float* bias;
   const float* Q;
   float* hn;
@@ -186,6 +225,7 @@ struct EpReadoutQ {
 
 // edge_to_node readout (GNN.py:106-107): hn = act([x | s] W_n^T + b_n)
 struct EpReadout {
+  static constexpr bool kSeg = false;
   const float* bias;
   float* hn;
   float* zn;  // nullptr for ReLU

@@ -175,7 +175,7 @@ struct B3NtShape {
   static constexpr int BPT = (BU4 + NT - 1) / NT;
   static constexpr int LDC = BN + 4;
   static constexpr size_t STAGE_BYTES = 3 * BU4 * 16;
-  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4;
+  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4;  // + EpLayerSeg's dst
   static constexpr size_t LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
 };
 
@@ -401,6 +401,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     pv[it] = ep.pre4(m0 + r, n0 + 4 * c4);
   }
   float* C = reinterpret_cast<float*>(b3_lds);
+  constexpr bool SEG = EP::kSeg;  // the epilogue also sums the tile's dst segments (EpLayerSeg)
+  int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG: dst of rows m0 - 1 .. m0 + BM
+  if constexpr (SEG) {
+    for (int q = tid; q < BM + 2; q += NT) {
+      const int r = m0 - 1 + q;
+      sd[q] = (r >= 0 && r < M) ? ep.dst_s[r] : -1 - (r >= M);  // distinct sentinels
+    }
+  }
 #pragma unroll
   for (int i = 0; i < RF; ++i)
 #pragma unroll
@@ -414,8 +422,49 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     const int q = tid + it * NT;
     if (q < BM * C4) {
       const int r = q / C4, c4 = q - r * C4;
-      const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
-      ep.apply4p(m0 + r, n0 + 4 * c4, v, pv[it], cx);
+      float4* cp = reinterpret_cast<float4*>(&C[r * S::LDC + 4 * c4]);
+      if constexpr (SEG)
+        *cp = ep.apply4p_h(m0 + r, n0 + 4 * c4, *cp, pv[it], cx);  // keep h for the sums
+      else
+        ep.apply4p(m0 + r, n0 + 4 * c4, *cp, pv[it], cx);
+    }
+  }
+  if constexpr (SEG) {
+    // a[v] = sum_{dst(i) = v} h[i] for the tile's columns (GNN.py:134): thread (16-row chunk,
+    // float4 column) sums, in row order, every segment that STARTS in its chunk (running past
+    // the chunk's end as needed), and the chunk-0 thread also the head segment begun in the
+    // previous tile.  A segment inside the tile is stored; one crossing a tile boundary is added
+    // atomically to a[v], which edge_init_segsum_fwd zeroed: with the two partials of a segment
+    // that spans two tiles the sum is order-independent (p + q == q + p), so the result is
+    // deterministic for every node of in-degree <= BM + 1.
+    __syncthreads();
+    const int nrow = min(BM, M - m0);
+    constexpr int NCH = BM / 16;
+    for (int q = tid; q < NCH * C4; q += NT) {
+      const int ch = q / C4, c4 = q - ch * C4;
+      const int col = n0 + 4 * c4;
+      if (col >= ep.N) continue;
+      int s = 16 * ch;
+      const int end = min(16 * ch + 16, nrow);
+      if (ch > 0)  // the tail of a segment begun in an earlier chunk belongs to that chunk
+        while (s < end && sd[s + 1] == sd[s]) ++s;
+      while (s < end) {
+        const int v = sd[s + 1];
+        float4 a = f4zero();
+        int r = s;
+        for (; r < nrow && sd[r + 1] == v; ++r)
+          a = f4add(a, *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]));
+        float* dst = ep.aout + (int64_t)v * ep.lda + col;
+        if ((s == 0 && sd[0] == v) || (r == nrow && sd[nrow + 1] == v)) {
+          atomicAdd(dst, a.x);
+          atomicAdd(dst + 1, a.y);
+          atomicAdd(dst + 2, a.z);
+          atomicAdd(dst + 3, a.w);
+        } else {
+          *reinterpret_cast<float4*>(dst) = a;
+        }
+        s = r;
+      }
     }
   }
 }

@@ -149,10 +149,17 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
   HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
 
+  // the layer GEMMs sum their dst segments in the epilogue (EpLayerSeg: one gather -> MLP ->
+  // segmented-reduce launch per layer) when the fused edge init zeroes what they accumulate
+  const bool fused_seg = Hp <= 512;
   if (Hp <= 512) {  // edge init + a_0 in one pass
     ProfScope _p("edge_init_seg_fwd", st);
+    SegZero z{};
+    z.n = D;
+    z.tile_rows = b3nt_rows(E, H);
+    for (int l = 0; l < D; ++l) z.a[l] = fv.a[l + 1];
     HIP_RET(edge_init_segsum_fwd(fv.P, iv.src_s, fv.e_s, Fe, d.Fep, fv.w0eT, b0, iv.dst_ptr, N,
-                                 H, Hp, d.act, fv.h[0], fv.pre[0], fv.a[0], st));
+                                 H, Hp, d.act, fv.h[0], fv.pre[0], fv.a[0], st, &z));
   } else {
     {
       ProfScope _p("edge_init_fwd", st);
@@ -175,13 +182,19 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
                d.act,    thresh,
                scale,    iv.rng,
                l};
-    {
-      ProfScope _p("gemm_nt_layer_fwd", st);
-      LdGatherDiff<false> al{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
-      HIP_RET(launch_b3nt(al, static_cast<const b3_u4*>(fv.b3lf[l]), ep, E, H, H, st));
+    LdGatherDiff<false> al{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
+    const b3_u4* img = static_cast<const b3_u4*>(fv.b3lf[l]);
+    if (fused_seg) {  // h_{l+1} and a_{l+1} = segsum_dst(h_{l+1}) from one launch
+      ProfScope _p("gemm_nt_layer_seg_fwd", st);
+      HIP_RET(launch_b3nt(al, img, EpLayerSeg{ep, iv.dst_s, fv.a[l + 1], Hp}, E, H, H, st));
+    } else {
+      {
+        ProfScope _p("gemm_nt_layer_fwd", st);
+        HIP_RET(launch_b3nt(al, img, ep, E, H, H, st));
+      }
+      ProfScope _p2("segsum_dst_fwd", st);
+      HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
     }
-    ProfScope _p2("segsum_dst_fwd", st);
-    HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
   }
 
   // readout: hn = act(s W_n[:, F:]^T + Q + b_n), s = a_D

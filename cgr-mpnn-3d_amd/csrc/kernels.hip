@@ -187,7 +187,7 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
     const float* __restrict__ P, const int* __restrict__ src_s, const float* __restrict__ e_s,
     int Fe, int Fep, const float* __restrict__ w0eT, const float* __restrict__ b0,
     const int* __restrict__ dst_ptr, int64_t N, int H, int Hp, int act, float* __restrict__ h0,
-    float* __restrict__ pre0, float* __restrict__ a) {
+    float* __restrict__ pre0, float* __restrict__ a, SegZero zero) {
   const int C4 = Hp >> 2;
   const int c = threadIdx.x;
   if (c >= C4) return;  // no barriers below
@@ -249,23 +249,34 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
       acc = f4add(acc, h);
     }
     *reinterpret_cast<float4*>(a + v * Hp + n) = acc;
+    if (zero.n > 0) {
+      const int ib = dst_ptr[v];
+      if (ie == ib || ib / zero.tile_rows != (ie - 1) / zero.tile_rows)
+        for (int l = 0; l < zero.n; ++l)
+          *reinterpret_cast<float4*>(zero.a[l] + v * Hp + n) = f4zero();
+    }
   }
 }
 
 hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
                                 int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
                                 int64_t N, int H, int Hp, int act, float* h0, float* pre0,
-                                float* a, hipStream_t st) {
+                                float* a, hipStream_t st, const SegZero* zero) {
   if (N <= 0) return hipSuccess;
   if (Hp % 4 || Hp / 4 > 128) return hipErrorInvalidValue;  // one thread per float4 column
+  SegZero z{};
+  if (zero) {
+    if (zero->n > 32 || zero->tile_rows <= 0) return hipErrorInvalidValue;
+    z = *zero;
+  }
   const int threads = (Hp / 4 + 63) / 64 * 64;
   const int nb = (int)cdiv(N, kEiNodes);
   if (Fe <= kEiMaxFe && (Fe == 0 || Fep % 4 == 0))
     hipLaunchKernelGGL(k_edge_init_seg<true>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
-                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a, z);
   else
     hipLaunchKernelGGL(k_edge_init_seg<false>, dim3(nb), dim3(threads), 0, st, P, src_s, e_s, Fe,
-                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a);
+                       Fep, w0eT, b0, dst_ptr, N, H, Hp, act, h0, pre0, a, z);
   return hipGetLastError();
 }
 

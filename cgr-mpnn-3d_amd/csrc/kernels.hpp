@@ -26,11 +26,19 @@ struct TransposeJobs {
 hipError_t transpose_batch(const TransposeJobs& jobs, hipStream_t st);
 
 // h0 = act(P[src_s] + e_s @ W0e^T + b0) ; pre0 stored if non-null
-// edge init + a_0 = segsum_dst(h0) in one pass (Hp <= 512); hipErrorInvalidValue otherwise
+// edge init + a_0 = segsum_dst(h0) in one pass (Hp <= 512); hipErrorInvalidValue otherwise.
+// `zero` (may be null): the rows of a_1 .. a_n the layer GEMMs' segmented-sum epilogue
+// (EpLayerSeg, row tiles of tile_rows) does not store -- nodes without in-edges and nodes whose
+// in-edges cross a tile boundary (accumulated atomically) -- are zeroed here.
+struct SegZero {
+  float* a[32];
+  int n;
+  int tile_rows;
+};
 hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e_s, int Fe,
                                 int Fep, const float* w0eT, const float* b0, const int* dst_ptr,
                                 int64_t N, int H, int Hp, int act, float* h0, float* pre0,
-                                float* a, hipStream_t st);
+                                float* a, hipStream_t st, const SegZero* zero = nullptr);
 hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int Fe, int Fep,
                          const float* w0eT, const float* b0, int64_t E, int H, int Hp, int act,
                          float* h0, float* pre0, hipStream_t st);
