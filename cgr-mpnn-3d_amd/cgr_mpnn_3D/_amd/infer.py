@@ -1,10 +1,13 @@
 """Batched inference.
 
 The reference evaluates one reaction at a time: ``test.py:85-113`` (DataLoader batch_size 1) and
-``cli_tool/activation_energy_predictor.py:71-80`` (per-graph loop, ``batch=None``).  Both work
-unchanged on the native module, but each call is a ~25-launch forward for ~30 atoms.  ``predict``
-runs the same eval-mode forward (dropout off, no autograd) over large device-collated batches
-(``GraphStore.collate``), so a whole test split is a handful of launches sequences.
+``cli_tool/activation_energy_predictor.py:71-80`` (per-graph loop, ``batch=None``), both under
+``torch.no_grad()`` in eval mode.  Both work unchanged on the native module, whose no-grad calls
+take the forward-only path (``cgr_gnn_predict``: no saved activations -- rings of two h and three
+a buffers -- and split-bf16 weight images packed once per parameter version,
+``functional.ImageCache``), but each call is still a ~20-launch forward for ~30 atoms.
+``predict`` runs that path over large device-collated batches (``GraphStore.collate``), so a whole
+test split is a handful of launch sequences.
 
     store = GraphStore.from_data_list(test_dataset, device)
     y_hat = predict(model, store, batch_size=4096)       # [num_graphs] on the device, in order

@@ -76,6 +76,14 @@ SIGNATURES = [
     ("cgr_gnn_backward", c_int32,
      [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
       c_int32, c_void_p, c_void_p, POINTER(c_void_p), c_void_p, POINTER(c_void_p), c_void_p]),
+    ("cgr_gnn_image_bytes", c_int64, [POINTER(CgrGnnConfig)]),
+    ("cgr_gnn_pack_images", c_int32, [POINTER(CgrGnnConfig), POINTER(c_void_p), c_void_p,
+                                      c_void_p]),
+    ("cgr_gnn_predict_arena_bytes", c_int64,
+     [POINTER(CgrGnnConfig), c_int64, c_int64, c_int64]),
+    ("cgr_gnn_predict", c_int32,
+     [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
+      c_void_p, c_int32, c_void_p, c_void_p, c_void_p, c_void_p]),
     ("cgr_segment_sum", c_int32,
      [c_void_p, c_int64, c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p]),
     ("cgr_dmpnn_conv_scratch_bytes", c_int64, [c_int64, c_int64, c_int64]),

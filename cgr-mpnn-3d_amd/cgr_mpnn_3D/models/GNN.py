@@ -31,7 +31,7 @@ import torch.nn.functional as F
 
 from .._amd import config as _config
 from .._amd import native
-from .._amd.functional import gnn_forward
+from .._amd.functional import ImageCache, gnn_forward, gnn_predict
 from .._amd.pool import global_add_pool, is_add_pool
 
 __all__ = ["GNN", "DMPNNConv", "global_add_pool"]
@@ -87,17 +87,32 @@ class GNN(nn.Module):
         if self.use_learnable_skip:
             self.skip_weights = nn.ParameterList(
                 nn.Parameter(torch.tensor(1.0)) for _ in range(self.depth))
-        # gradient-bucket hook (RCCL all-reduce), set by cgr_mpnn_3D._amd.ddp
-        self._grad_bucket_hook = None
-        # device dropout counter: the native forward advances it, so a HIP-graph-captured
-        # training step draws a fresh dropout mask per replay (non-persistent: state_dict keys
-        # stay the reference's)
-        self.register_buffer("_cgr_rng_counter", torch.zeros(1, dtype=torch.int64),
-                             persistent=False)
-        GNN._cgr_instances += 1
-        self._cgr_instance = GNN._cgr_instances
+        self._cgr_native_state()
 
     _cgr_instances = 0  # construction order salts the dropout key (two models, distinct masks)
+
+    def _cgr_native_state(self):
+        """State of the native path that the reference module does not have (filled in for
+        modules unpickled from a reference checkpoint, test.py:94 / trainer.py:208 save whole
+        modules)."""
+        if not hasattr(self, "_grad_bucket_hook"):
+            # gradient-bucket hook (RCCL all-reduce), set by cgr_mpnn_3D._amd.ddp
+            self._grad_bucket_hook = None
+        if "_cgr_rng_counter" not in self._buffers:
+            # device dropout counter: the native forward advances it, so a HIP-graph-captured
+            # training step draws a fresh dropout mask per replay (non-persistent: state_dict
+            # keys stay the reference's)
+            self.register_buffer("_cgr_rng_counter", torch.zeros(1, dtype=torch.int64),
+                                 persistent=False)
+        if not hasattr(self, "_cgr_instance"):
+            GNN._cgr_instances += 1
+            self._cgr_instance = GNN._cgr_instances
+        if not hasattr(self, "_cgr_images"):
+            self._cgr_images = ImageCache()  # forward weight images of the no-grad path
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        self._cgr_native_state()
 
     def _cgr_dropout_seed(self, dev) -> int:
         """Base of the dropout key: the seed of ``dev``'s CUDA generator (what torch.manual_seed
@@ -196,10 +211,16 @@ class GNN(nn.Module):
         counter = self._cgr_rng_counter
         if counter.device != dev:
             counter = self._cgr_rng_counter = counter.to(dev)
-        return gnn_forward((F_, Fe, H, self.depth, act, self.use_learnable_skip), x, edge_index,
-                           edge_attr, batch, graph_ptr, num_graphs, drop, seed, training,
-                           [p.contiguous() for p in params], self._grad_bucket_hook,
-                           rng_counter=counter)
+        cfg = (F_, Fe, H, self.depth, act, self.use_learnable_skip)
+        params = [p.contiguous() for p in params]
+        if not (torch.is_grad_enabled() and any(p.requires_grad for p in params)):
+            # no gradient wanted (test.py / the CLI run under torch.no_grad()): the forward-only
+            # path, no saved activations, weight images cached across calls
+            return gnn_predict(cfg, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, drop,
+                               seed, training, [p.detach() for p in params], self._cgr_images,
+                               rng_counter=counter)
+        return gnn_forward(cfg, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, drop,
+                           seed, training, params, self._grad_bucket_hook, rng_counter=counter)
 
 
 class DMPNNConv(nn.Module):

@@ -34,7 +34,9 @@ static int forward_flags(const void* arena) {
 
 int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
                      const float* dropout_p, uint64_t seed, uint64_t* rng_counter, int training,
-                     void* arena, float* y, hipStream_t st);
+                     void* arena, float* y, hipStream_t st, const FwdMode& mode);
+hipError_t pack_forward_images(const Dims& d, const float* const* params, const ImageLayout& IL,
+                               void* images, hipStream_t st);
 int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
                       const float* dropout_p, uint64_t seed, int training, const void* arena,
                       const float* dy, float* const* grads, void* workspace,
@@ -69,10 +71,8 @@ struct Bump {
 constexpr size_t kNone = (size_t)-1;
 }  // namespace
 
-ArenaLayout arena_layout(const Dims& d) {
-  ArenaLayout L;
-  memset(&L, 0xff, sizeof(L));
-  Bump b;
+// index bookkeeping, sorted edge features and the x-GEMM outputs: shared by both layouts
+static void layout_prefix(const Dims& d, ArenaLayout& L, Bump& b) {
   const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
   // zero block: six int arrays back to back, padded to a multiple of 16 bytes
   L.zero_block = b.off;
@@ -102,6 +102,14 @@ ArenaLayout arena_layout(const Dims& d) {
   L.P = b.take(4 * N * Hp);
   L.Q = b.take(4 * N * Hp);
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
+}
+
+ArenaLayout arena_layout(const Dims& d) {
+  ArenaLayout L;
+  memset(&L, 0xff, sizeof(L));
+  Bump b;
+  const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
+  layout_prefix(d, L, b);
   L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
   L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
   L.b3rob = b.take(16 * b3_img_u4(d.H, d.H));
@@ -120,6 +128,37 @@ ArenaLayout arena_layout(const Dims& d) {
   L.bytes = b.off;
   L.off_index_begin = 0;
   return L;
+}
+
+ArenaLayout eval_arena_layout(const Dims& d) {
+  ArenaLayout L;
+  memset(&L, 0xff, sizeof(L));
+  Bump b;
+  const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
+  layout_prefix(d, L, b);
+  const size_t h0 = b.take(4 * E * Hp);
+  const size_t hr[2] = {d.D >= 2 ? b.take(4 * E * Hp) : kNone, b.take(4 * E * Hp)};
+  const size_t ar[3] = {b.take(4 * N * Hp), b.take(4 * N * Hp),
+                        d.D >= 2 ? b.take(4 * N * Hp) : kNone};
+  for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
+    L.h[l] = l > d.D ? kNone : (l == 0 ? h0 : hr[l & 1]);
+    L.a[l] = l > d.D ? kNone : ar[l % 3];
+  }
+  L.hn = b.take(4 * N * Hp);
+  L.g = b.take(4 * B * Hp);
+  L.bytes = b.off;
+  L.off_index_begin = 0;
+  return L;
+}
+
+ImageLayout image_layout(const Dims& d) {
+  ImageLayout I;
+  Bump b;
+  I.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
+  I.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
+  for (int l = 0; l < CGR_MAX_DEPTH; ++l) I.b3lf[l] = l < d.D ? b.take(16 * b3_img_u4(d.H, d.H)) : kNone;
+  I.bytes = b.off;
+  return I;
 }
 
 static inline void* at(void* base, size_t off) {
@@ -342,7 +381,7 @@ int cgr_gnn_forward(const cgr_gnn_config* cfg, const float* const* params, const
   const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
   note_forward(arena, -1);  // not usable by a backward unless the forward below succeeds
   const int r = gnn_forward_impl(d, params, b, dropout_p, seed, rng_counter, training, arena, y,
-                                 (hipStream_t)stream);
+                                 (hipStream_t)stream, FwdMode{});
   if (r == 0) note_forward(arena, training);
   return r;
 }
@@ -379,6 +418,52 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, cons
   return gnn_backward_impl(d, params, b, dropout_p, seed, training, arena, dy, grads, workspace,
                            reinterpret_cast<hipEvent_t const*>(bucket_events),
                            (hipStream_t)stream);
+}
+
+int64_t cgr_gnn_image_bytes(const cgr_gnn_config* cfg) {
+  if (validate_config(cfg)) return -1;
+  return (int64_t)image_layout(make_dims(cfg, 1, 2, 1)).bytes;
+}
+
+int cgr_gnn_pack_images(const cgr_gnn_config* cfg, const float* const* params, void* images,
+                        void* stream) {
+  clear_stale_hip_error();
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  CGR_CHECK(params != nullptr && images != nullptr, "cgr: params / images must not be NULL");
+  const int np = cgr_gnn_num_params(cfg);
+  for (int i = 0; i < np; ++i) CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
+  const Dims d = make_dims(cfg, 1, 2, 1);
+  HIP_RET(pack_forward_images(d, params, image_layout(d), images, (hipStream_t)stream));
+  return 0;
+}
+
+int64_t cgr_gnn_predict_arena_bytes(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
+  if (validate_config(cfg)) return -1;
+  return (int64_t)eval_arena_layout(make_dims(cfg, N, E, B)).bytes;
+}
+
+int cgr_gnn_predict(const cgr_gnn_config* cfg, const float* const* params, const cgr_batch* b,
+                    const float* dropout_p, uint64_t seed, uint64_t* rng_counter,
+                    int32_t training, const void* images, void* arena, float* y, void* stream) {
+  clear_stale_hip_error();
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  rc = validate_batch(cfg, b);
+  if (rc) return rc;
+  CGR_CHECK(params != nullptr && images != nullptr && arena != nullptr && y != nullptr,
+            "cgr: params / images / arena / y must not be NULL");
+  CGR_CHECK((training & ~CGR_TRAIN_DROPOUT) == 0,
+            "cgr_gnn_predict: `training` may only hold CGR_TRAIN_DROPOUT (no backward follows)");
+  const int np = cgr_gnn_num_params(cfg);
+  for (int i = 0; i < np; ++i) CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
+  const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
+  FwdMode m;
+  m.eval = true;
+  m.images = images;
+  note_forward(arena, -1);  // never a backward's arena
+  return gnn_forward_impl(d, params, b, dropout_p, seed, rng_counter, training, arena, y,
+                          (hipStream_t)stream, m);
 }
 
 int cgr_segment_sum(const float* values, int64_t ld_values, const int32_t* index,

@@ -127,6 +127,7 @@ struct EpLayerSeg : EpLayer {
   const int* dst_s;  // [M] node of each (dst-sorted) row
   float* aout;       // [nodes, lda]; crossing / empty segments zeroed beforehand
   int64_t lda;
+  float* znext;      // or null: [nodes, lda] whose crossing segments this GEMM zeroes (eval ring)
   // apply4p that also returns the stored h (rows / columns outside: v unchanged)
   __device__ __forceinline__ float4 apply4p_h(int r, int c, float4 v, const Pre& p,
                                               const Ctx& cx) const {

@@ -455,7 +455,10 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         for (; r < nrow && sd[r + 1] == v; ++r)
           a = f4add(a, *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]));
         float* dst = ep.aout + (int64_t)v * ep.lda + col;
-        if ((s == 0 && sd[0] == v) || (r == nrow && sd[nrow + 1] == v)) {
+        const bool head = s == 0 && sd[0] == v, tail = r == nrow && sd[nrow + 1] == v;
+        if (tail && !head && ep.znext)  // the tile where a crossing segment starts
+          *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + col) = f4zero();
+        if (head || tail) {
           atomicAdd(dst, a.x);
           atomicAdd(dst + 1, a.y);
           atomicAdd(dst + 2, a.z);

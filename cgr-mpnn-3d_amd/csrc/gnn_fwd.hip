@@ -43,12 +43,45 @@ void dropout_params(const float* dropout_p, int training, int l, uint32_t* thres
   dropout_consts(dropout_p, training, l, thresh, scale);
 }
 
+// every forward weight image (x-GEMM, readout, layers) into `images` (ImageLayout), one launch
+hipError_t pack_forward_images(const Dims& d, const float* const* params, const ImageLayout& IL,
+                               void* images, hipStream_t st) {
+  const int H = d.H, F = d.F, Fe = d.Fe, D = d.D;
+  const float* W0 = params[CGR_PARAM_EDGE_INIT_W];
+  const float* Wn = params[CGR_PARAM_E2N_W(D)];
+  char* base = static_cast<char*>(images);
+  B3PackJobs pj{};
+  hipError_t e;
+  if (F > 0) {
+    b3_u4* ximg = reinterpret_cast<b3_u4*>(base + IL.b3x);
+    const B3Cols cx = b3_cols(2 * H);
+    if ((e = b3_pack_add(pj, B3PackJob{W0, F + Fe, 1, ximg, 0, H, H, F, cx.nimg, b3_nk(F)}, st)))
+      return e;
+    if ((e = b3_pack_add(pj, B3PackJob{Wn, F + H, 1, ximg, H, cx.nimg - H, H, F, cx.nimg,
+                                       b3_nk(F)}, st)))
+      return e;
+  }
+  if ((e = b3_pack_add(pj, b3_job(Wn + F, F + H, 1, H, H, base + IL.b3rof), st))) return e;
+  for (int l = 0; l < D; ++l)
+    if ((e = b3_pack_add(pj, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, base + IL.b3lf[l]),
+                         st)))
+      return e;
+  return b3_pack(pj, st);
+}
+
 int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
                      const float* dropout_p, uint64_t seed, uint64_t* rng_counter, int training,
-                     void* arena, float* y, hipStream_t st) {
-  const ArenaLayout L = arena_layout(d);
+                     void* arena, float* y, hipStream_t st, const FwdMode& mode) {
+  const ArenaLayout L = mode.eval ? eval_arena_layout(d) : arena_layout(d);
   const IndexView iv = index_view(arena, L);
-  const FloatView fv = float_view(arena, L, d);
+  FloatView fv = float_view(arena, L, d);
+  if (mode.eval) {  // forward images from the caller (cgr_gnn_pack_images)
+    const ImageLayout IL = image_layout(d);
+    char* im = static_cast<char*>(const_cast<void*>(mode.images));
+    fv.b3x = d.F > 0 ? im + IL.b3x : nullptr;
+    fv.b3rof = im + IL.b3rof;
+    for (int l = 0; l < d.D; ++l) fv.b3lf[l] = im + IL.b3lf[l];
+  }
   const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
   const float* W0 = params[CGR_PARAM_EDGE_INIT_W];
   const float* b0 = params[CGR_PARAM_EDGE_INIT_B];
@@ -95,7 +128,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   // layer / readout images (forward, and backward unless this is an eval forward) on the caller's
   // stream ahead of graph prep (that chain has slack beside the x-GEMM chain, and the layers
   // that read them run there)
-  if (F > 0) {
+  if (F > 0 && !mode.eval) {
     ProfScope _p("weight_pack", side);
     B3PackJobs pj{};
     const B3Cols cx = b3_cols(2 * H);
@@ -105,7 +138,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
                                       H, F, cx.nimg, b3_nk(F)}, side));
     HIP_RET(b3_pack(pj, side));
   }
-  {
+  if (!mode.eval) {
     ProfScope _p("weight_pack", st);
     B3PackJobs pm{};
     HIP_RET(b3_pack_add(pm, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof), st));
@@ -154,10 +187,12 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   const bool fused_seg = Hp <= 512;
   if (Hp <= 512) {  // edge init + a_0 in one pass
     ProfScope _p("edge_init_seg_fwd", st);
+    // the entries the layer epilogues accumulate: every a_l (training), or the first two
+    // buffers of the eval ring (each layer l >= 1 re-zeroes a_{l+2}'s, see below)
     SegZero z{};
-    z.n = D;
+    z.n = mode.eval ? (D < 2 ? D : 2) : D;
     z.tile_rows = b3nt_rows(E, H);
-    for (int l = 0; l < D; ++l) z.a[l] = fv.a[l + 1];
+    for (int l = 0; l < z.n; ++l) z.a[l] = fv.a[l + 1];
     HIP_RET(edge_init_segsum_fwd(fv.P, iv.src_s, fv.e_s, Fe, d.Fep, fv.w0eT, b0, iv.dst_ptr, N,
                                  H, Hp, d.act, fv.h[0], fv.pre[0], fv.a[0], st, &z));
   } else {
@@ -186,7 +221,11 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     const b3_u4* img = static_cast<const b3_u4*>(fv.b3lf[l]);
     if (fused_seg) {  // h_{l+1} and a_{l+1} = segsum_dst(h_{l+1}) from one launch
       ProfScope _p("gemm_nt_layer_seg_fwd", st);
-      HIP_RET(launch_b3nt(al, img, EpLayerSeg{ep, iv.dst_s, fv.a[l + 1], Hp}, E, H, H, st));
+      // eval ring: a_{l+2} reuses a_{l-1}'s buffer, free once layer l-1 read it; this layer
+      // zeroes the entries layer l+1 will accumulate there
+      float* znext = (mode.eval && l >= 1 && l + 2 <= D) ? fv.a[l + 2] : nullptr;
+      HIP_RET(launch_b3nt(al, img, EpLayerSeg{ep, iv.dst_s, fv.a[l + 1], Hp, znext}, E, H, H,
+                          st));
     } else {
       {
         ProfScope _p("gemm_nt_layer_fwd", st);

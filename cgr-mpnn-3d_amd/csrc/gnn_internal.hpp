@@ -118,8 +118,24 @@ struct WorkspaceLayout {
   int dsig_blocks;
 };
 
+// Forward variants.  Training (cgr_gnn_forward): every activation the backward reads is saved in
+// the arena and the weight images are packed into it by each call.  Eval (cgr_gnn_predict): no
+// saved activations -- h_1.. h_D alias a two-buffer ring and a_0 .. a_D a three-buffer ring (the
+// fused layer epilogue zeroes the entries it accumulates two layers ahead, gnn_fwd.hip) -- and
+// the forward weight images come packed from the caller (cgr_gnn_pack_images), reused across
+// calls until the parameters change.
+struct FwdMode {
+  bool eval = false;
+  const void* images = nullptr;
+};
+struct ImageLayout {
+  size_t b3x, b3rof, b3lf[CGR_MAX_DEPTH], bytes;
+};
+ImageLayout image_layout(const Dims& d);
+
 Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B);
 ArenaLayout arena_layout(const Dims& d);
+ArenaLayout eval_arena_layout(const Dims& d);
 WorkspaceLayout workspace_layout(const Dims& d);
 IndexView index_view(void* arena, const ArenaLayout& L);
 FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d);

@@ -148,6 +148,24 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params,
                      int32_t training, const void* arena, const float* dy, float* const* grads,
                      void* workspace, void* const* bucket_events, void* stream);
 
+/* Forward-only inference (test.py:85-113 and cli_tool/activation_energy_predictor.py:70-80 run
+ * GNN.forward under torch.no_grad() in eval mode).  cgr_gnn_predict computes exactly what
+ * cgr_gnn_forward computes for `y`, but keeps no activation for a backward (h_1 .. h_D share a
+ * two-buffer ring and a_0 .. a_D a three-buffer one: its arena is ~half the training arena) and
+ * takes the split-bf16 forward weight images pre-packed by cgr_gnn_pack_images into `images`
+ * (cgr_gnn_image_bytes bytes, caller-owned): pack once, predict many batches, re-pack only when
+ * the parameters change.  `training` may only hold CGR_TRAIN_DROPOUT (module in train mode under
+ * no_grad).  Sizes: cgr_gnn_predict_arena_bytes. */
+int64_t cgr_gnn_image_bytes(const cgr_gnn_config* cfg);
+int cgr_gnn_pack_images(const cgr_gnn_config* cfg, const float* const* params, void* images,
+                        void* stream);
+int64_t cgr_gnn_predict_arena_bytes(const cgr_gnn_config* cfg, int64_t num_nodes,
+                                    int64_t num_edges, int64_t num_graphs);
+int cgr_gnn_predict(const cgr_gnn_config* cfg, const float* const* params,
+                    const cgr_batch* batch, const float* dropout_p, uint64_t seed,
+                    uint64_t* rng_counter, int32_t training, const void* images, void* arena,
+                    float* y, void* stream);
+
 /* Segmented sum, the sum-scatter primitive of the path (PyG propagate aggr="add", GNN.py:134;
  * global_add_pool, GNN.py:110) over a CSR: out[s, :] = sum_{j in [seg_ptr[s], seg_ptr[s+1])}
  * values[index ? index[j] : j, :].  width = row length in floats; ld_* = row strides (floats).

@@ -69,3 +69,22 @@ def test_pickle_roundtrip_keeps_class_paths(tmp_path):
     assert type(m2).__module__ == "cgr_mpnn_3D.models.GNN"
     for (k1, v1), (k2, v2) in zip(m.state_dict().items(), m2.state_dict().items()):
         assert k1 == k2 and torch.equal(v1, v2)
+
+
+def test_unpickling_a_reference_style_module_fills_native_state(tmp_path):
+    # a checkpoint saved by the reference (trainer.py:208 pickles the whole module) has none of
+    # the native path's private state; unpickling into this class must add it
+    import torch
+
+    from cgr_mpnn_3D.models.GNN import GNN
+
+    m = GNN(20, 4, depth=2, hidden_sizes=[8, 8])
+    for k in ("_grad_bucket_hook", "_cgr_instance", "_cgr_images"):
+        del m.__dict__[k]
+    del m._buffers["_cgr_rng_counter"]
+    p = tmp_path / "ref_style.pth"
+    torch.save(m, p)
+    m2 = torch.load(p, weights_only=False)  # our own test file
+    assert m2._grad_bucket_hook is None and m2._cgr_images is not None
+    assert "_cgr_rng_counter" in m2._buffers and isinstance(m2._cgr_instance, int)
+    assert set(m2.state_dict()) == set(m.state_dict())
