@@ -945,10 +945,12 @@ hipError_t b3_eimage(const float* x, int64_t ld, int64_t R, int C, b3_u4* img, h
 //   * compute wave w: n-fragments w, w + CW, ... (RN of them, all TNK k-fragments each) plus RX
 //     of the remaining (TNN % CW) x TNK products, dealt round-robin; its A fragments come straight
 //     from the e-image, one step ahead of the MFMAs (two register sets, loop unrolled by 2).
-//   * staging waves: the k-side operand B (TNK x 16 columns of the tile), as gemm_b3tn_kernel
-//     stages it (4 columns x one 8-row chunk per job, split into hi / lo, transposed into LDS),
-//     its loads issued a whole interval before they are staged and the gather's index loads one
-//     more interval ahead; chunk c = rows 8 c .. 8 c + 7 of the step, the e-image's order.
+//   * staging waves: the k-side operand B (TNK x 16 columns of the tile), split into hi / lo and
+//     transposed into LDS in the NT image geometry (chunk c of a column = rows 8 c .. 8 c + 7 of
+//     the step, the e-image's order); a job is 4 columns x 4 rows (one 8-byte half of a chunk
+//     per column and piece), so the split's VALU is spread over SW = 3 waves on three SIMDs
+//     (8-row jobs on 1.25 waves: lab 40 us);  its loads are issued a whole interval before they
+//     are staged and the gather's index loads one more interval ahead.
 //   * one barrier per step: compute reads LDS buffer t & 1 while staging fills (t + 1) & 1.
 //   * splits start on 32-row boundaries, so a split's last step reads only its own rows or the
 //     image's zero rows: A is never masked; B rows past R read row 0 (finite, times zero A).
@@ -959,7 +961,8 @@ template <int TNN, int TNK>
 struct B3TniShape {
   static constexpr int CW = 8;
   static constexpr int BC = TNK * 16;
-  static constexpr int JB = BC;  // staging jobs (4 columns x one 8-row chunk; one per column)
+  static constexpr int JC = BC / 4;  // 4-column groups
+  static constexpr int JB = JC * 8;  // staging jobs: 4 columns x 4 rows (half an 8-row chunk)
   static constexpr int SW = (JB + 63) / 64;
   static constexpr int NT = (CW + SW) * 64;
   static constexpr int RN = TNN / CW;
@@ -989,27 +992,31 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
 
   if (w >= CW) {
     // ================= staging waves: B of step t + 1 into LDS buffer (t + 1) & 1 =============
+    // job (4-column group cg, 4-row group hc): rows 4 hc .. 4 hc + 3 of a step, half of the
+    // 16-byte chunk hc / 2 of each column (the e-image's row order); lanes run column groups
+    // fastest, so a load instruction covers ~3 rows x 320 contiguous bytes
+    constexpr int JC = S::JC;
     const int q = tid - CW * 64;
     const bool act = q < JB;
-    const int jc = q & 3;                     // chunk: rows 8 jc .. 8 jc + 7 of a step
-    const int jcol = (act ? q >> 2 : 0) * 4;  // first of the job's 4 columns in the tile
+    const int hc = act ? q / JC : 0;
+    const int jcol = (act ? q - hc * JC : 0) * 4;  // first of the job's 4 columns in the tile
     const int gcol = k0 + jcol;
     const float* base0 = TB::base(bl, 0, gcol);
     const float* base1 = TB::base(bl, 1, gcol);
-    float4 raw[16];  // (NL = 8 operand kinds use the first 8)
+    float4 raw[16];  // rows j < 4: a / plain rows in raw[j], gathered h rows in raw[8 + j]
     uint32_t off[TB::NL];
-    int ix[8][2];
+    int ix[4][2];
     auto rowof = [&](int t, int j) {
-      const int e = e_begin + t * 32 + 8 * jc + j;
+      const int e = e_begin + t * 32 + 4 * hc + j;
       return e < R ? e : 0;
     };
     auto index = [&](int t) {  // the gather's index loads of step t
 #pragma unroll
-      for (int j = 0; j < 8; ++j) TB::idx(bl, rowof(t, j), ix[j]);
+      for (int j = 0; j < 4; ++j) TB::idx(bl, rowof(t, j), ix[j]);
     };
     auto fetch = [&]() {  // addresses from the last index(), then the data loads
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int h = 0; h < TB::NL / 8; ++h) off[8 * h + j] = TB::off(bl, ix[j], h, gcol, Kout);
 #ifdef CGR_TNI_LAB
@@ -1019,19 +1026,22 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
       }
 #endif
 #pragma unroll
-      for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const float4*>(base0 + off[i]);
+      for (int i = 0; i < 4; ++i) raw[i] = *reinterpret_cast<const float4*>(base0 + off[i]);
       if constexpr (TB::NL == 16) {
 #pragma unroll
-        for (int i = 8; i < 16; ++i) raw[i] = *reinterpret_cast<const float4*>(base1 + off[i]);
+        for (int i = 8; i < 12; ++i) raw[i] = *reinterpret_cast<const float4*>(base1 + off[i]);
       }
     };
-    auto put = [&](b3_u4* img, int t, const float (&f)[8]) {
-      b3_u4 pc[2];
-      b3_split8<2>(f, pc);
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    auto put = [&](b3_u4* img, int t, float f0, float f1, float f2, float f3) {
+      float a0, a1, a2, a3, c0, c1, c2, c3;
+      const uint32_t h01 = b3_cvt2(f0, f1, a0, a1), h23 = b3_cvt2(f2, f3, a2, a3);
+      const uint32_t l01 = b3_cvt2(f0 - a0, f1 - a1, c0, c1), l23 = b3_cvt2(f2 - a2, f3 - a3, c2, c3);
       const int row = b3tn_sigma(jcol + t);
-      const int slot = jc ^ lds_swz(row);
-      img[row * 4 + slot] = pc[0];
-      img[(BC + row) * 4 + slot] = pc[1];
+      const int slot = (hc >> 1) ^ lds_swz(row);
+      char* b = reinterpret_cast<char*>(img) + 8 * (hc & 1);
+      *reinterpret_cast<u2v*>(b + (row * 4 + slot) * 16) = u2v{h01, h23};
+      *reinterpret_cast<u2v*>(b + ((BC + row) * 4 + slot) * 16) = u2v{l01, l23};
     };
     auto stage = [&](int buf) {
       b3_u4* img = b3_lds + buf * SU4;
@@ -1041,18 +1051,14 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
         return;
       }
 #endif
-      float4 u[8];
+      float4 u[4];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) u[j] = TB::get(raw, j);
+      for (int j = 0; j < 4; ++j) u[j] = TB::get(raw, j);
       if (act) {
-        const float f0[8] = {u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x};
-        const float f1[8] = {u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y};
-        const float f2[8] = {u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z};
-        const float f3[8] = {u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w};
-        put(img, 0, f0);
-        put(img, 1, f1);
-        put(img, 2, f2);
-        put(img, 3, f3);
+        put(img, 0, u[0].x, u[1].x, u[2].x, u[3].x);
+        put(img, 1, u[0].y, u[1].y, u[2].y, u[3].y);
+        put(img, 2, u[0].z, u[1].z, u[2].z, u[3].z);
+        put(img, 3, u[0].w, u[1].w, u[2].w, u[3].w);
       }
     };
     if (nt > 0) {
