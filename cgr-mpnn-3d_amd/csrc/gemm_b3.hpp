@@ -949,8 +949,8 @@ hipError_t b3_eimage(const float* x, int64_t ld, int64_t R, int C, b3_u4* img, h
 //     transposed into LDS in the NT image geometry (chunk c of a column = rows 8 c .. 8 c + 7 of
 //     the step, the e-image's order); a job is 4 columns x 4 rows (one 8-byte half of a chunk
 //     per column and piece), so the split's VALU is spread over SW = 3 waves on three SIMDs
-//     (8-row jobs on 1.25 waves: lab 40 us);  its loads are issued a whole interval before they
-//     are staged and the gather's index loads one more interval ahead.
+//     (8-row jobs on 1.25 waves: lab 40 us);  its loads are issued two intervals before they are
+//     staged (two register sets) and the gather's index loads one more interval ahead.
 //   * one barrier per step: compute reads LDS buffer t & 1 while staging fills (t + 1) & 1.
 //   * splits start on 32-row boundaries, so a split's last step reads only its own rows or the
 //     image's zero rows: A is never masked; B rows past R read row 0 (finite, times zero A).
@@ -1003,7 +1003,8 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
     const int gcol = k0 + jcol;
     const float* base0 = TB::base(bl, 0, gcol);
     const float* base1 = TB::base(bl, 1, gcol);
-    float4 raw[16];  // rows j < 4: a / plain rows in raw[j], gathered h rows in raw[8 + j]
+    // two register sets: rows j < 4 of a / plain rows in r[j], gathered h rows in r[8 + j]
+    float4 raw0[16], raw1[16];
     uint32_t off[TB::NL];
     int ix[4][2];
     auto rowof = [&](int t, int j) {
@@ -1014,7 +1015,7 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
 #pragma unroll
       for (int j = 0; j < 4; ++j) TB::idx(bl, rowof(t, j), ix[j]);
     };
-    auto fetch = [&]() {  // addresses from the last index(), then the data loads
+    auto fetch = [&](float4 (&raw)[16]) {  // addresses from the last index(), then the loads
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1043,7 +1044,7 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
       *reinterpret_cast<u2v*>(b + (row * 4 + slot) * 16) = u2v{h01, h23};
       *reinterpret_cast<u2v*>(b + ((BC + row) * 4 + slot) * 16) = u2v{l01, l23};
     };
-    auto stage = [&](int buf) {
+    auto stage = [&](const float4 (&raw)[16], int buf) {
       b3_u4* img = b3_lds + buf * SU4;
 #ifdef CGR_TNI_LAB
       if (CGR_TNI_LAB & 8) {
@@ -1063,18 +1064,25 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
     };
     if (nt > 0) {
       index(0);
-      fetch();  // step 0
+      fetch(raw0);  // step 0
       index(1);
-      stage(0);
-      fetch();  // step 1
+      fetch(raw1);  // step 1
       index(2);
+      stage(raw0, 0);
+      fetch(raw0);  // step 2
+      index(3);
       __syncthreads();
-      // interval t (compute on step t): stage step t + 1, whose loads were issued one interval
-      // ago, then issue step t + 2's (index loads a further interval ahead)
-      for (int t = 0; t < nt; ++t) {
-        if (t + 1 < nt) stage((t + 1) & 1);
-        fetch();  // step t + 2
-        index(t + 3);
+      // interval t (compute on step t): stage step t + 1, whose loads were issued two intervals
+      // ago, then issue step t + 3's into the freed set (index loads one interval ahead of them)
+      for (int t = 0; t < nt; t += 2) {
+        if (t + 1 < nt) stage(raw1, 1);
+        fetch(raw1);  // step t + 3
+        index(t + 4);
+        __syncthreads();
+        if (t + 1 >= nt) break;
+        if (t + 2 < nt) stage(raw0, 0);
+        fetch(raw0);  // step t + 4
+        index(t + 5);
         __syncthreads();
       }
     }

@@ -26,13 +26,15 @@ from collections import defaultdict
 
 def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
     n = name
-    if "gemm_b3tn_kernel" in n:  # split-bf16 TN (gemm_b3.hpp)
+    if "gemm_b3tni_kernel" in n or "gemm_b3tn_kernel" in n:  # split-bf16 TN (gemm_b3.hpp)
         if "LdGatherDiff" in n:
             return "gemm_tn_wgrad_layer"
         if "LdConcat" in n:
             return "gemm_tn_wgrad_readout"
         return "gemm_tn_wgrad_node"
     if "gemm_b3nt_kernel" in n:  # split-bf16 NT
+        if "EpLayerSeg" in n:
+            return "gemm_nt_layer_seg_fwd"
         if "EpLayer" in n:
             return "gemm_nt_layer_fwd"
         if "EpSplit2" in n:
@@ -41,17 +43,17 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
             return "gemm_nt_readout_fwd"
         if "EpStore" in n:  # E-row layer GEMM on 8-wave tiles, N-row readout on 4-wave tiles
             return "gemm_nt_readout_bwd" if "gemm_b3nt_kernel<4," in n else "gemm_nt_layer_bwd"
+    if "k_b3_eimage" in n:
+        return "eimage"
     if "k_b3_pack" in n:
         return "weight_pack"
-    if "gemm_rs_kernel" in n:
-        return "gemm_nt_layer_fwd" if "EpLayer" in n else "gemm_nt_layer_bwd"
-    if "gemm_tnr_kernel" in n:
+    if "gemm_tnr_kernel" in n:  # register-direct fp32 TN (shapes the split-bf16 TN does not take)
         if "TnrDiff" in n:
             return "gemm_tn_wgrad_layer"
         if "TnrConcat" in n:
             return "gemm_tn_wgrad_readout"
         return "gemm_tn_wgrad_node"
-    if "gemm_tn_kernel" in n:
+    if "gemm_tn_kernel" in n:  # fp32 fallback tiles (shapes the split-bf16 TN does not take)
         if "LdGatherDiff" in n:
             return "gemm_tn_wgrad_layer"
         if "LdConcat" in n:
@@ -61,15 +63,6 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
         if m and m.group(1) != "4":
             return "gemm_tn_wgrad_node"
         return "gemm_tn_wgrad_edge"  # ambiguous only when F % 4 == 0; see note in the output
-    if "gemm_nt_kernel" in n:
-        if "EpLayer" in n:
-            return "gemm_nt_layer_fwd"
-        if "EpSplit2" in n:
-            return "gemm_nt_x"
-        if "EpReadout" in n:
-            return "gemm_nt_readout_fwd"
-        if "EpStore" in n:  # dm = dpre W (E rows) vs ds = dzn W_n (N rows): larger grid is E
-            return "gemm_nt_layer_bwd" if grid == max(grids_by_name[n]) else "gemm_nt_readout_bwd"
     if "k_segsum_act_bwd" in n:
         return "segsum_act_bwd"
     if "k_segsum" in n:
