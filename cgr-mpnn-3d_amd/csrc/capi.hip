@@ -220,7 +220,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   WorkspaceLayout W;
   Bump b;
   const size_t N = (size_t)d.N, E = (size_t)d.E, Hp = (size_t)d.Hp;
-  for (int l = 0; l < 2; ++l) W.dpre[l] = b.take(4 * E * Hp);
+  W.dpre = b.take(4 * E * Hp * (size_t)d.D);  // one per layer (gnn_bwd.hip)
   W.dm = b.take(4 * E * Hp);
   W.dh0 = b.take(4 * E * Hp);
   W.dzn = b.take(4 * N * Hp);

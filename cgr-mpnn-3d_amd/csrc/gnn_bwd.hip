@@ -102,8 +102,6 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   const FloatView fv = float_view(const_cast<void*>(arena), L, d);
   const WorkspaceLayout WL = workspace_layout(d);
   char* ws = static_cast<char*>(workspace);
-  // dpre of layer l: ring buffer l & 1 (gnn_internal.hpp)
-  auto dpre = [&](int l) { return reinterpret_cast<float*>(ws + WL.dpre[l & 1]); };
   float* dm = reinterpret_cast<float*>(ws + WL.dm);
   float* dh0 = reinterpret_cast<float*>(ws + WL.dh0);
   float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
@@ -118,6 +116,12 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   void* img_main = ws + WL.img_main;
 
   const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
+  // dpre of layer l: a buffer per layer, so that writing dpre_{l-1} never waits for the side
+  // stream's weight gradient of layer l+1 (a cross-queue edge on the critical chain of a
+  // captured step: ~5 us each)
+  auto dpre = [&](int l) {
+    return reinterpret_cast<float*>(ws + WL.dpre) + (int64_t)l * E * Hp;
+  };
 
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
@@ -215,7 +219,6 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
     return la;
   };
-  hipEvent_t tn_done[CGR_MAX_DEPTH];
   if (D > 0) {  // top layer: dh_D = ds[dst]
     ProfScope _p("layer_act_bwd", st);
     HIP_RET(layer_act_bwd(layer_args(D - 1), nb, st));
@@ -254,7 +257,6 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       } else {
         HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, slab, bslab, true, &p, side));
       }
-      HIP_RET(record_point(ss, side, &tn_done[l]));
       HIP_RET(tn_reduce(p, slab, bslab, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
                         grads[CGR_PARAM_CONV_B(l)], side));
       if (bucket_events) HIP_RET(hipEventRecord(bucket_events[D - l], side));
@@ -263,8 +265,6 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     // dh_l = da[dst] - dm[rev] -> dpre_{l-1} (or dpre0 of the edge init when l == 0)
     ProfScope _p("segsum_act_bwd", st);
     if (l > 0) {
-      // ring: dpre buffer (l-1) & 1 was last read by the weight gradient of layer l+1
-      if (l + 1 <= D - 1) HIP_RET(hipStreamWaitEvent(st, tn_done[l + 1], 0));
       HIP_RET(segsum_act_bwd(layer_args(l - 1), iv.src_list, iv.src_ptr, iv.dst_ptr, N, false,
                              iv.status, st));
     } else {

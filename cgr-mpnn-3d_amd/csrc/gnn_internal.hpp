@@ -110,7 +110,7 @@ struct ArenaLayout {
 // main-stream nodes onto the side stream's queue)
 struct WorkspaceLayout {
   size_t bytes;
-  size_t dpre[2], dm, dh0, dzn, ds, Gs, slab, bslab, slab2, bslab2, dsig_part, slab_elems,
+  size_t dpre, dm, dh0, dzn, ds, Gs, slab, bslab, slab2, bslab2, dsig_part, slab_elems,
       bslab_elems;
   // split-bf16 e-images (gemm_b3.hpp B3EImg) of the weight gradients' shared operand: dpre_l and
   // dzn on the side stream (one at a time), Gs on the caller's stream
