@@ -104,10 +104,11 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("gemm_tn_wgrad_readout", 1, 2.0 * N * H * (F + H),
         f4 * (N * H + N * F + N * H + H * (F + H) + H))
     add("gemm_nt_readout_bwd", 1, 2.0 * N * H * H, f4 * (N * H + H * H + N * H))
-    add("layer_act_bwd", 1, 0.0, f4 * (N * H + 4 * E * H) + i4 * E)  # top layer: dh = ds[dst]
-    # da = segsum_src(dm) fused with the layer below's activation backward (D - 1 launches) or the
-    # edge-init backward (1): dm once, h_{l+1} mask, dh0 read + write, dpre write (+ indices)
-    add("segsum_act_bwd", D, 2.0 * E * H, f4 * (5 * E * H) + i4 * (2 * E + 2 * (N + 1)))
+    add("layer_act_bwd", 1, 0.0, f4 * (N * H + 2 * E * H) + i4 * E)  # top layer: dh = ds[dst]
+    # da = segsum_src(dm) fused with the layer below's activation backward (D - 1 launches: dm once,
+    # h_{l+1} mask, dpre write) or the edge-init backward (1: dm, h_0 mask, the D layers' dpre
+    # summed into dh0, dpre0 write); per launch on average 4 E*H floats (+ indices)
+    add("segsum_act_bwd", D, 2.0 * E * H, f4 * (4 * E * H) + i4 * (2 * E + 2 * (N + 1)))
     add("gemm_tn_wgrad_layer", D, 2.0 * E * H * H,
         f4 * (E * H + N * H + E * H + H * H + H) + 2 * i4 * E)
     add("gemm_nt_layer_bwd", D, 2.0 * E * H * H, f4 * (E * H + H * H + E * H))

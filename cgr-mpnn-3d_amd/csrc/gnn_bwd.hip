@@ -7,18 +7,18 @@
 //   dW_n = dzn^T [x | s], db_n = colsum(dzn), ds = dzn W_n[:, F:]
 //   dh_D = ds[dst]
 //   for l = D-1 .. 0:
-//     dpre = dh_{l+1} * mask * act'(pre_l) ; dh0 += s_l dpre ; ds_l = sum dpre*h0
+//     dpre_l = dh_{l+1} * mask * act'(pre_l) ; ds_l = sum dpre_l*h0
 //     dW_l = dpre^T (a_l[src] - h_l[rev])  (message recomputed, never stored) ; db_l = colsum
 //     dm = dpre W_l ; da = segsum_src(dm) ; dh_l = da[dst] - dm[rev]  (one fused kernel with the
 //     next lower layer's dpre, da never stored: k_segsum_act_bwd)
-//   dpre0 = (dh0 + dh_0) * act'(pre0)
+//   dh0 = sum_l s_l dpre_l (every layer's skip term) ; dpre0 = (dh0 + dh_0) * act'(pre0)
 //   dW0[:, F:] = dpre0^T e ; db0 = colsum(dpre0) ; dW0[:, :F] = (segsum_src dpre0)^T x
 //
 // Streams: the critical path is act_bwd -> dm GEMM -> segsum per layer.  Every weight-gradient
 // TN GEMM (+ its slab reduction) only feeds the gradient outputs, so it runs on the side stream,
-// forked right after its input is produced; dpre is double-buffered so the next layer's act_bwd
-// can proceed, and the main stream waits for the side stream only before re-using a dpre buffer
-// and at the very end.
+// forked right after its input is produced; every layer's dpre has a buffer of its own (the
+// edge-init backward sums them into dh0), so the main stream waits for the side stream only at
+// the very end.
 #include "dispatch.hpp"
 #include "epilogues.hpp"
 #include "gnn_internal.hpp"
@@ -210,12 +210,10 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.scale = scale;
     la.layer = l;
     la.act = d.act;
-    la.first = (l == D - 1);
     la.E = E;
     la.H = H;
     la.Hp = Hp;
     la.dpre = dpre(l);
-    la.dh0 = dh0;
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
     return la;
   };
@@ -223,7 +221,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     ProfScope _p("layer_act_bwd", st);
     HIP_RET(layer_act_bwd(layer_args(D - 1), nb, st));
   }
-  // edge init: dpre0 overwrites dh0 in place (each element read then written by one thread)
+  // edge init: dpre0 = (dh0 + dh_0) * act'(pre0), dh0 summed from the layers' dpre buffers,
+  // written to the dh0 buffer
   float* dpre0 = dh0;
   for (int l = D - 1; l >= 0; --l) {
     float* dp = dpre(l);  // written by the previous iteration's fused kernel (or just above)
@@ -279,6 +278,10 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       le.Hp = Hp;
       le.dh0 = dh0;
       le.dpre = dpre0;
+      le.dpre_all = dpre(0);
+      le.dpre_stride = (int64_t)E * Hp;
+      le.nlayers = D;
+      for (int k = 0; k < D; ++k) le.sig[k] = d.learnable_skip ? params[CGR_PARAM_SKIP(D, k)] : nullptr;
       HIP_RET(segsum_act_bwd(le, iv.src_list, iv.src_ptr, iv.dst_ptr, N, true, iv.status, st));
     }
   }

@@ -436,7 +436,8 @@ hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_gra
 int layer_act_bwd_blocks(int64_t E, int Hp) { return (int)cdiv(E * (Hp / 4), 256); }
 
 // one float4 of one edge row of the layer backward, given dh = dL/dh_{l+1}[i, n..n+3]:
-// dpre = dh * keep/(1-p) * act'(pre) ; dh0 (+)= sigma * dpre ; dsig += dpre . h0
+// dpre = dh * keep/(1-p) * act'(pre) ; dsig += dpre . h0  (dh0 = sum_l sigma_l dpre_l is formed
+// by the edge-init backward from the per-layer dpre buffers)
 __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
                                               uint64_t key, float& dsig) {
   const int64_t o = i * a.Hp + n;
@@ -460,15 +461,6 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
   }
   const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
   *reinterpret_cast<float4*>(a.dpre + o) = dp;
-  {
-    const float sg = a.sigma ? a.sigma[0] : 1.f;
-    float4 acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
-    acc.x += sg * dp.x;
-    acc.y += sg * dp.y;
-    acc.z += sg * dp.z;
-    acc.w += sg * dp.w;
-    *reinterpret_cast<float4*>(a.dh0 + o) = acc;
-  }
   if (a.dsig_part) {
     const float4 h0 = *reinterpret_cast<const float4*>(a.h0 + o);
     const float hz[4] = {h0.x, h0.y, h0.z, h0.w};
@@ -476,29 +468,6 @@ __device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, 
     for (int k = 0; k < 4; ++k)
       if (n + k < a.H) dsig += d[k] * hz[k];
   }
-}
-
-// one float4 of one edge row of the edge-init backward (GNN.py:85-87 reversed), in place over dh0:
-// dpre0 = (dh0 + dh_1) * act'(pre0)
-__device__ __forceinline__ void edge_init_bwd_row(const LayerBwdArgs& a, int64_t i, int n,
-                                                  float4 dh) {
-  const int64_t o = i * a.Hp + n;
-  const float4 s0 = *reinterpret_cast<const float4*>(a.dh0 + o);
-  float4 d = f4add(s0, dh);
-  if (a.act == ACT_RELU) {
-    const float4 h = *reinterpret_cast<const float4*>(a.h0 + o);
-    d.x = h.x > 0.f ? d.x : 0.f;
-    d.y = h.y > 0.f ? d.y : 0.f;
-    d.z = h.z > 0.f ? d.z : 0.f;
-    d.w = h.w > 0.f ? d.w : 0.f;
-  } else {
-    const float4 z = *reinterpret_cast<const float4*>(a.pre + o);
-    d.x *= act_grad(z.x, a.act);
-    d.y *= act_grad(z.y, a.act);
-    d.z *= act_grad(z.z, a.act);
-    d.w *= act_grad(z.w, a.act);
-  }
-  *reinterpret_cast<float4*>(a.dpre + o) = d;
 }
 
 __device__ __forceinline__ void block_partial(float v, float* dst) {
@@ -536,7 +505,7 @@ hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st) {
 // edge_init_bwd_row given the same values.
 struct RowOps {
   float4 m;    // h_{l+1} (ReLU mask) or pre (other activations); edge init: h_0 or pre_0
-  float4 acc;  // dh0 before this layer's accumulation (layer) / dh0 (edge init)
+  float4 acc;  // edge init: dh0 = sum_l sigma_l dpre_l
   float4 h0;   // h_0 (learnable-skip partials)
 };
 
@@ -544,7 +513,7 @@ __device__ __forceinline__ RowOps layer_row_loads(const LayerBwdArgs& a, int64_t
   const int64_t o = i * a.Hp + n;
   RowOps r;
   r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.hnext : a.pre) + o);
-  r.acc = a.first ? f4zero() : *reinterpret_cast<const float4*>(a.dh0 + o);
+  r.acc = f4zero();
   r.h0 = a.dsig_part ? *reinterpret_cast<const float4*>(a.h0 + o) : f4zero();
   return r;
 }
@@ -570,15 +539,6 @@ __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i
   }
   const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
   *reinterpret_cast<float4*>(a.dpre + o) = dp;
-  {
-    const float sg = a.sigma ? a.sigma[0] : 1.f;
-    float4 acc = r.acc;
-    acc.x += sg * dp.x;
-    acc.y += sg * dp.y;
-    acc.z += sg * dp.z;
-    acc.w += sg * dp.w;
-    *reinterpret_cast<float4*>(a.dh0 + o) = acc;
-  }
   if (a.dsig_part) {
     const float hz[4] = {r.h0.x, r.h0.y, r.h0.z, r.h0.w};
 #pragma unroll
@@ -587,11 +547,22 @@ __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i
   }
 }
 
+// dh0 = sum_l sigma_l dpre_l (GNN.py:97: every layer adds sigma_l h0), summed from the top layer
+// down, one sigma-weighted float4 per layer buffer
 __device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
   const int64_t o = i * a.Hp + n;
   RowOps r;
   r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.h0 : a.pre) + o);
-  r.acc = *reinterpret_cast<const float4*>(a.dh0 + o);
+  float4 acc = f4zero();
+  for (int l = a.nlayers - 1; l >= 0; --l) {
+    const float sg = a.sig[l] ? a.sig[l][0] : 1.f;
+    const float4 dp = *reinterpret_cast<const float4*>(a.dpre_all + l * a.dpre_stride + o);
+    acc.x += sg * dp.x;
+    acc.y += sg * dp.y;
+    acc.z += sg * dp.z;
+    acc.w += sg * dp.w;
+  }
+  r.acc = acc;
   r.h0 = f4zero();
   return r;
 }

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "cgr_mpnn3d.h"  // CGR_MAX_DEPTH
+
 namespace cgr {
 
 // out[s, :w] = sum_{j in [ptr[s], ptr[s+1])} vals[idx ? idx[j] : j, :w]
@@ -72,19 +74,24 @@ struct LayerBwdArgs {
   float scale;
   int layer;
   int act;
-  int first;
   int64_t E;
   int H, Hp;
   float* dpre;
-  float* dh0;         // written (first) or accumulated (sigma-weighted dpre of every layer)
+  float* dh0;         // edge init: dpre0 (written in place of dh0, the buffer it names)
   float* dsig_part;   // [gridDim] partial sums of dpre*h0 (nullable)
+  // edge init: dh0 = sum_l sigma_l dpre_l over the layers' dpre buffers (dpre_l at
+  // dpre_all + l * dpre_stride), summed l = D-1 .. 0; sig[l] nullptr -> 1
+  const float* dpre_all;
+  int64_t dpre_stride;
+  int nlayers;
+  const float* sig[CGR_MAX_DEPTH];
 };
 // nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
 hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);
 int layer_act_bwd_blocks(int64_t E, int Hp);
 // da = segsum_src(dm) (never stored) fused with the layer backward of every edge row i whose
 // dst is the segment's node (dh = da[dst(i)] - dm[rev(i)]), or with the edge-init backward
-// (edge_init: a.dh0 -> a.dpre in place, a.h0 / a.pre = h_0 / pre_0).  With learnable-skip
+// (edge_init: dh0 from the layers' dpre buffers -> a.dpre, a.h0 / a.pre = h_0 / pre_0).  With learnable-skip
 // partials it launches segsum_act_bwd_blocks(E, N, Hp) blocks (size dsig_part accordingly).
 // status: graph prep's status word (bit 2 clear: paired edges, the fast form; see kernels.hip)
 hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int* src_ptr,
@@ -92,7 +99,6 @@ hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int*
                           hipStream_t st);
 int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp);
 
-// dpre0 = (dh0 + da[dst_s] - dm[rev_s]) * act'(pre0)   (ReLU: h0 > 0)
 // dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
 // gap_len > 0: slab columns [gap_at, gap_at + gap_len) are padding and skipped; later columns
 // shift down by gap_len in dst (the x | s concat of the readout with x padded to 4 floats)
