@@ -486,10 +486,11 @@ inline hipError_t launch_b3nt_t(const AL& al, const b3_u4* Bimg, int nimg, const
   return hipGetLastError();
 }
 
-// workgroup rows: 8 waves (128 rows) when that still gives ~200+ workgroups, else 4 (64 rows)
+// workgroup rows: 8 waves (128 rows) when that still gives ~100+ workgroups (the node-row readout
+// GEMMs at 120 x 8 waves beat 240 x 4 waves at one wave per SIMD: step A/B +0.8 %), else 4 (64 rows)
 inline int b3nt_waves(int M, int N) {
   const int tiles_n = b3_cols(N).tiles;
-  return ((M + 127) / 128) * tiles_n >= 192 ? 8 : 4;
+  return ((M + 127) / 128) * tiles_n >= 96 ? 8 : 4;
 }
 
 // rows per workgroup tile of launch_b3nt for an M x N GEMM

@@ -129,18 +129,21 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
   hipStream_t side = (prof_enabled() || single_stream()) ? st : ss->side;
 
-  // head + readout
+  // readout (the head's dwf / dbf sums run on the side stream below)
   {
     ProfScope _p("head_readout_bwd", st);
-    HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
-                     grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], st));
     HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
                             Hp, d.act, dzn, st));
   }
-  // side: dW_n = dzn^T [x | s], db_n (forked before the main stream's readout NT: deferring it
-  // behind a layer, or enqueuing the NT first, A/B -4..-14 %)
+  // side: dwf, dbf; dW_n = dzn^T [x | s], db_n (forked before the main stream's readout NT:
+  // deferring it behind a layer, or enqueuing the NT first, A/B -4..-14 %)
   {
     HIP_RET(fork_to(ss, st, side));
+    {  // dwf = dy^T g, dbf: off the main chain (step A/B +0.8 %)
+      ProfScope _p("head_readout_bwd", side);
+      HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
+                       grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], side));
+    }
     TnPlan p;
     if (fv.xp) {  // [xp | s] with x padded to Fp: the pad columns are skipped by the reduce
       const int Fp = d.Fp;
@@ -180,7 +183,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       HIP_RET(tn_reduce(p, slab, bslab, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
                         grads[CGR_PARAM_E2N_B(D)], side));
     }
-    // bucket 0 (edge_to_node, ffn): the side stream forked after head_bwd wrote the ffn grads
+    // bucket 0 (edge_to_node, ffn): both written on the side stream above
     if (bucket_events) HIP_RET(hipEventRecord(bucket_events[0], side));
   }
   // main: ds = dzn W_n[:, F:]
