@@ -115,8 +115,9 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("segsum_src_bwd", 1, E * H, seg_dst + i4 * E)  # Gs = segsum_src(dpre0) for dW0[:, :F]
     add("gemm_tn_wgrad_edge", 1, 2.0 * E * H * Fe, f4 * (E * H + E * Fe + H * Fe + H))
     add("gemm_tn_wgrad_node", 1, 2.0 * N * H * F, f4 * (N * H + N * F + H * F))
-    # e-images of the weight gradients' shared operand (dpre_l, dzn, Gs): fp32 in, 2 bf16 out
-    add("eimage", D + 2, 0.0, f4 * (D * E * H + 2 * N * H) * 2 / (D + 2))
+    # e-images of the weight gradients' shared operand (dpre_l, dzn): fp32 in, 2 bf16 out (Gs's
+    # is written by segsum_src_bwd itself)
+    add("eimage", D + 1, 0.0, f4 * (D * E * H + N * H) * 2 / (D + 1))
     # split-bf16 weight images, once per step: fp32 weights in, three bf16 pieces out
     nw = 2 * H * F + (2 + 2 * D) * H * H
     add("weight_pack", 1, 0.0, (f4 + 3 * 2.0) * nw)

@@ -94,4 +94,58 @@ hipError_t b3_eimage(const float* x, int64_t ld, int64_t R, int C, b3_u4* img, h
   return hipGetLastError();
 }
 
+// e-image of the segmented sum G[v, :C] = sum_{j in [ptr[v], ptr[v+1])} X[idx[j], :C] (the node
+// weight gradient's Gs = segsum_src(dpre0), gnn_bwd.hip) without G ever reaching memory.  Block =
+// one 32-row step s x 64 columns: the sums (thread = (row, float4 column), the segment's rows in
+// order, as k_segsum_v4 adds them) go to an LDS tile [32][65], then thread = (column, 8-row chunk),
+// chunk fastest, splits its 8 values and writes the two 16-byte chunk slots (a wave's stores cover
+// 16 consecutive 64-byte slots).  Rows >= R and columns >= C are written as 0.
+constexpr int kSegImgCols = 64;
+__global__ __launch_bounds__(256) void k_b3_segsum_eimage(const float* __restrict__ x, int64_t ld,
+                                                          const int* __restrict__ idx,
+                                                          const int* __restrict__ ptr, int64_t R,
+                                                          int C, int cimg,
+                                                          b3_u4* __restrict__ img) {
+  __shared__ float tile[32][kSegImgCols + 1];
+  const int64_t s = blockIdx.y;
+  const int c0 = blockIdx.x * kSegImgCols;
+  for (int it = threadIdx.x; it < 32 * (kSegImgCols / 4); it += blockDim.x) {
+    const int r = it / (kSegImgCols / 4), c4 = it - r * (kSegImgCols / 4);
+    const int64_t v = s * 32 + r;
+    const int c = c0 + 4 * c4;
+    float4 acc = f4zero();
+    if (v < R && c < C) {
+      const float* base = x + c;
+      for (int j = ptr[v], e = ptr[v + 1]; j < e; ++j)
+        acc = f4add(acc, *reinterpret_cast<const float4*>(base + (int64_t)idx[j] * ld));
+    }
+    const float a[4] = {acc.x, acc.y, acc.z, acc.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) tile[r][4 * c4 + k] = (c + k < C) ? a[k] : 0.f;
+  }
+  __syncthreads();
+  const int q = threadIdx.x & 3, cl = threadIdx.x >> 2;  // 64 columns x 4 chunks
+  const int c = c0 + cl;
+  if (c >= cimg) return;
+  float f[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = tile[8 * q + j][cl];
+  b3_u4 pc[2];
+  b3_split8<2>(f, pc);
+  img[((s * 2 + 0) * cimg + c) * 4 + q] = pc[0];
+  img[((s * 2 + 1) * cimg + c) * 4 + q] = pc[1];
+}
+
+hipError_t b3_segsum_eimage(const float* x, int64_t ld, const int* idx, const int* ptr, int64_t R,
+                            int C, b3_u4* img, hipStream_t st) {
+  const int64_t steps = (R + 31) / 32;
+  const int cimg = b3_eimg_cols(C);
+  if (steps <= 0 || C <= 0) return hipSuccess;
+  if ((ld & 3) || ld < (C + 3) / 4 * 4 || ((uintptr_t)x & 15)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_b3_segsum_eimage, dim3((cimg + kSegImgCols - 1) / kSegImgCols,
+                                              (unsigned)steps), dim3(256), 0, st, x, ld, idx, ptr,
+                     R, C, cimg, img);
+  return hipGetLastError();
+}
+
 }  // namespace cgr

@@ -940,6 +940,10 @@ inline size_t b3_eimg_bytes(int64_t R, int C) {
   return (size_t)((R + 31) / 32) * 2 * (size_t)b3_eimg_cols(C) * 64;
 }
 hipError_t b3_eimage(const float* x, int64_t ld, int64_t R, int C, b3_u4* img, hipStream_t st);
+// e-image of G = segsum(X) over the CSR (idx, ptr) of R segments, G never stored (b3_pack.hip);
+// X rows 16-byte aligned with ld >= round_up(C, 4)
+hipError_t b3_segsum_eimage(const float* x, int64_t ld, const int* idx, const int* ptr, int64_t R,
+                            int C, b3_u4* img, hipStream_t st);
 
 // Workgroup = CW = 8 compute waves + SW staging waves (warp-specialised: a wave runs one role for
 // the whole kernel, so the registers of the two roles are not live together).

@@ -58,6 +58,17 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
 // split-bf16 TN with the n-side operand A [R, Nout] as an e-image (gemm_b3.hpp): A is split
 // once by b3_eimage into `img`, then every k-tile of the GEMM reads it pre-split
 template <class BL>
+static hipError_t b3tni_run(const char* name, const void* img, const BL& bl, int Nout, int Kout,
+                            int R, float* slab, float* bslab, bool want_bias, TnPlan* plan,
+                            hipStream_t st, int target = kB3TnTarget) {
+  const B3TnPlan q = b3tn_plan(Nout, Kout, R, target);
+  *plan = TnPlan{1, q.tiles_k, q.splits, q.rows_per_split};
+  ProfScope _p(name, st);
+  return launch_b3tni(B3EImg{static_cast<const b3_u4*>(img), b3_eimg_cols(Nout)}, bl, q, slab,
+                      bslab, Nout, Kout, R, want_bias, st);
+}
+
+template <class BL>
 static hipError_t b3tni_gemm(const char* name, const float* A, int64_t lda, void* img,
                              const BL& bl, int Nout, int Kout, int R, float* slab, float* bslab,
                              bool want_bias, TnPlan* plan, hipStream_t st,
@@ -67,11 +78,7 @@ static hipError_t b3tni_gemm(const char* name, const float* A, int64_t lda, void
     const hipError_t e = b3_eimage(A, lda, R, Nout, static_cast<b3_u4*>(img), st);
     if (e != hipSuccess) return e;
   }
-  const B3TnPlan q = b3tn_plan(Nout, Kout, R, target);
-  *plan = TnPlan{1, q.tiles_k, q.splits, q.rows_per_split};
-  ProfScope _p(name, st);
-  return launch_b3tni(B3EImg{static_cast<const b3_u4*>(img), b3_eimg_cols(Nout)}, bl, q, slab,
-                      bslab, Nout, Kout, R, want_bias, st);
+  return b3tni_run(name, img, bl, Nout, Kout, R, slab, bslab, want_bias, plan, st, target);
 }
 
 // split-bf16 TN (gemm_b3.hpp); same slab layout as tn_gemm
@@ -310,19 +317,25 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     const int rc = edge_tn();
     if (rc) return rc;
   }
-  {
-    ProfScope _p("segsum_src_bwd", st);
-    HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, Hp, Gs, Hp, st));
-  }
-  if (F > 0) {  // main: dW0[:, :F] = Gs^T x (own slab: runs beside the side stream's work)
+  if (F > 0) {  // main: dW0[:, :F] = Gs^T x, Gs = segsum_src(dpre0) (own slab: beside the side
+                // stream's work)
     const float* xb = fv.xp ? fv.xp : b->x;
     const int64_t ldx = fv.xp ? d.Fp : F;
     TnPlan p;
     const int Fx = fv.xp ? d.Fp : F;  // x columns the GEMM covers (pad columns are zero)
     const LdPlain<4> gbl{xb, ldx};
-    if (ldx % 4 == 0 && ((uintptr_t)xb & 15) == 0 && b3tni_ok(gbl, H, N)) {
-      HIP_RET(b3tni_gemm("gemm_tn_wgrad_node", Gs, Hp, img_main, gbl, H, Fx, N, slab2, bslab2,
-                         Fe == 0, &p, st, kB3TnNodeTarget));
+    const bool b3 = ldx % 4 == 0 && ((uintptr_t)xb & 15) == 0 && b3tni_ok(gbl, H, N);
+    if (b3) {  // Gs straight into the TN's e-image (never stored in fp32)
+      ProfScope _p("segsum_src_bwd", st);
+      HIP_RET(b3_segsum_eimage(dpre0, Hp, iv.src_list, iv.src_ptr, N, H,
+                               static_cast<b3_u4*>(img_main), st));
+    } else {
+      ProfScope _p("segsum_src_bwd", st);
+      HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, Hp, Gs, Hp, st));
+    }
+    if (b3) {
+      HIP_RET(b3tni_run("gemm_tn_wgrad_node", img_main, gbl, H, Fx, N, slab2, bslab2, Fe == 0, &p,
+                        st, kB3TnNodeTarget));
       // the flat reduce: this one ends the backward's main chain
       HIP_RET(tn_reduce(p, slab2, bslab2, H, Fx, gW0, F + Fe, 0, Fe > 0 ? nullptr : gb0, st, F,
                         Fx - F, true));
