@@ -100,7 +100,9 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("gemm_nt_readout_fwd", 1, 2.0 * N * H * H, f4 * (N * H + N * H + H * H + H + 2 * N * H))
     add("pool_head_fwd", 1, 2.0 * N * H, f4 * (N * H + B * H + H + B) + i4 * (B + 1))
     # backward
-    add("head_readout_bwd", 1, 2.0 * N * H, f4 * (B + 2 * N * H + B * H + 2 * H + N * H))
+    add("head_bwd", 1, 2.0 * B * H, f4 * (B + B * H + 2 * H))  # dwf = dy^T g, dbf
+    # dzn = dy[graph] wf * act'(zn): hn (ReLU mask) read, dzn written (+ the da zeroing it carries)
+    add("readout_act_bwd", 1, 0.0, f4 * (B + H + 2 * N * H) + i4 * N)
     add("gemm_tn_wgrad_readout", 1, 2.0 * N * H * (F + H),
         f4 * (N * H + N * F + N * H + H * (F + H) + H))
     add("gemm_nt_readout_bwd", 1, 2.0 * N * H * H, f4 * (N * H + H * H + N * H))

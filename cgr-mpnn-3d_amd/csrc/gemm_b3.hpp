@@ -536,40 +536,13 @@ namespace cgr {
 // Two-piece split (x = hi + lo, hi = bf16(x), lo = bf16(x - hi)) and three terms per product
 // (lo.hi, hi.lo, hi.hi; the dropped lo.lo and the residuals are <= 2^-16 |ab| per product, and a
 // weight gradient sums ~10^4 of them with independent signs: fp32-level error against the fp64
-// oracle, profiles/r02_split_precision_experiment.txt "b3t").
-//   * one workgroup owns ALL TNN n-fragments of the output (Nout <= 16 TNN) and TNK k-fragments
-//     over one split (a range of e rows); wave w owns n-fragments w, w + WAVES, ... (fragments
-//     past TNN compute clamped data and are discarded: every wave runs RN of them) and all TNK
-//     k-fragments.
-//   * per 32-row step both operands are staged transposed into LDS as bf16 hi/lo pieces:
-//     [piece][column row][4 swizzled 16-byte chunks of 8 e-rows] (the NT image geometry), so every
-//     fragment read is one conflict-free ds_read_b128.  A staging job = 4 columns x the 8 rows of
-//     one chunk: per row one float4 (two for the gathered difference: a[src] and h[rev]).  Lanes
-//     run chunk fastest, then column groups, so one load instruction covers 4 rows x 256
-//     contiguous bytes (whole cache lines).  Column c is stored at row sigma(c), a rotation inside
-//     its 16-column block, so the 16 lanes of a b128 store pass hit four different 64-byte bank
-//     groups; a fragment still reads one 1 KB block.
-//   * jobs: A (n side) on threads [0, JA = 16 TNN), B (k side) on [JA, JA + 16 TNK); the bias
-//     gradient (column sums of A) is accumulated by the A stagers from the fp32 values.
-//   * pipeline: step t + 1's loads are in flight across step t's MFMAs (a sched_barrier keeps
-//     the compiler from sinking them), addressed one step ahead from index loads issued two steps
-//     ahead (ahead of the data loads, so waiting for the data covers them).
-template <int TNN, int TNK>
-struct B3TnShape {
-  static constexpr int AC = TNN * 16, BC = TNK * 16, COLS = AC + BC;
-  static constexpr int JA = AC, JOBS = AC + BC;  // 4-column jobs x 4 chunks = one job per column
-  static constexpr int WAVES = (JOBS + 63) / 64 < 8 ? 8 : (JOBS + 63) / 64;
-  static constexpr int NT = WAVES * 64;
-  // wave w: n-fragments w, w + WAVES, ... (RN full rows of TNK products) plus RX of the
-  // remaining (TNN % WAVES) x TNK fragment products, dealt round-robin
-  static constexpr int RN = TNN / WAVES;
-  static constexpr int REM = (TNN % WAVES) * TNK;
-  static constexpr int RX = (REM + WAVES - 1) / WAVES;
-  static constexpr int SU4 = 2 * COLS * 4;  // b3_u4 per stage buffer
-  static constexpr size_t LDS_BYTES = (size_t)2 * SU4 * 16 + (size_t)4 * AC * 4;
-  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
-};
-
+// oracle, profiles/r02_split_precision_experiment.txt "b3t").  The kernel (gemm_b3tni_kernel,
+// below) takes A pre-split as an e-image and stages B transposed into LDS in the NT image
+// geometry ([piece][column row][4 swizzled 16-byte chunks of 8 e-rows]: every fragment read one
+// conflict-free ds_read_b128; column c stored at row sigma(c), a rotation inside its 16-column
+// block, so a b128 store pass hits four 64-byte bank groups).  Plans: one workgroup per (split of
+// the e rows, k-tile of TNK fragments), all Nout columns (TNN n-fragments) per workgroup; splits
+// start on 32-row boundaries.
 struct B3TnPlan {
   int tiles_k, splits, rows_per_split, tnn;
 };
@@ -654,271 +627,15 @@ struct B3TnSrc<LdGatherDiff<X>> {  // a[src] - h[rev]: loads 0..7 the a rows, 8.
   static bool fits(const LdGatherDiff<X>& l, int R) { return (double)R * l.ld < 4.0e9; }
 };
 
-template <int TNN, int TNK, class AL, class BL>
-__global__ __launch_bounds__((B3TnShape<TNN, TNK>::NT)) void gemm_b3tn_kernel(
-    AL al, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout, int R,
-    int rows_per_split, int tiles_k, int want_bias) {
-  typedef B3TnSrc<AL> TA;
-  typedef B3TnSrc<BL> TB;
-  static_assert(TA::NL == 8, "A is a row operand");
-  using S = B3TnShape<TNN, TNK>;
-  constexpr int NT = S::NT, WAVES = S::WAVES, RN = S::RN, RX = S::RX, AC = S::AC, COLS = S::COLS;
-  constexpr int SU4 = S::SU4, JA = S::JA, JOBS = S::JOBS;
-  extern __shared__ b3_u4 b3_lds[];
-  float* bpart = reinterpret_cast<float*>(b3_lds + 2 * SU4);  // [4 chunks][AC]
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = lin / tiles_k, tkk = lin - split * tiles_k;
-  const int k0 = tkk * TNK * 16;
-  const int e_begin = split * rows_per_split;
-  const int e_end = min(R, e_begin + rows_per_split);
-  const int nt = e_end > e_begin ? (e_end - e_begin + 31) / 32 : 0;
-  const int rrow = b3tn_sigma(fr);  // fragment reads: storage row of column fr of a block
-  const int sw = fg ^ lds_swz(rrow);
-  const bool do_bias = want_bias && tkk == 0;
-
-  // ---- this thread's staging job ----
-  const bool wa = tid < JA;
-  const bool act = tid < JOBS;
-  const int qa = wa ? tid : tid - JA;
-  const int jc = qa & 3;           // chunk: rows b3_kperm(jc, 0..7) of a step
-  const int jcol = (qa >> 2) * 4;  // first of the job's 4 columns in the operand's tile
-  const int gcol = wa ? jcol : k0 + jcol;
-  const int lcol = wa ? jcol : AC + jcol;  // logical LDS column (multiple of 4)
-  const int kin = wa ? Nout : Kout;
-  const float* base0 = wa ? TA::base(al, 0, gcol) : TB::base(bl, 0, gcol);
-  const float* base1 = wa ? TA::base(al, 1, gcol) : TB::base(bl, 1, gcol);
-  float4 raw[16];
-  uint32_t off[16];
-  int ix[8][2];
-  float bsum[4] = {0.f, 0.f, 0.f, 0.f};
-
-  auto rowof = [&](int t, int j) {
-    const int e = e_begin + t * 32 + b3_kperm(jc, j);
-    return e < R ? e : 0;
-  };
-  auto index = [&](int t) {  // the gather's index loads of step t (B stagers only)
-    if (!wa)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) TB::idx(bl, rowof(t, j), ix[j]);
-  };
-  auto address = [&](int t) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      int ra[2];
-      TA::idx(al, rowof(t, j), ra);
-#pragma unroll
-      for (int h = 0; h < TB::NL / 8; ++h)
-        off[8 * h + j] = wa ? TA::off(al, ra, h, gcol, kin) : TB::off(bl, ix[j], h, gcol, kin);
-    }
-  };
-  auto fetch = [&]() {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) raw[i] = *reinterpret_cast<const float4*>(base0 + off[i]);
-    if constexpr (TB::NL == 16) {
-      if (!wa)
-#pragma unroll
-        for (int i = 8; i < 16; ++i) raw[i] = *reinterpret_cast<const float4*>(base1 + off[i]);
-    }
-  };
-  // column lcol + t, 8 rows -> two pieces -> storage row sigma, slot chunk ^ swizzle
-  auto put = [&](b3_u4* img, int t, const float (&f)[8]) {
-    b3_u4 pc[2];
-    b3_split8<2>(f, pc);
-    const int row = b3tn_sigma(lcol + t);
-    const int slot = jc ^ lds_swz(row);
-    img[row * 4 + slot] = pc[0];
-    img[(COLS + row) * 4 + slot] = pc[1];
-  };
-  // A rows past the split are zeroed (their products vanish whatever B holds there); columns
-  // past Nout / Kout land in discarded outputs
-  auto stage = [&](int t, int buf) {
-    const int e0 = e_begin + t * 32;
-    b3_u4* img = b3_lds + buf * SU4;
-    float4 u[8];
-    if (wa) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float keep = e0 + b3_kperm(jc, j) < e_end ? 1.f : 0.f;
-        const float4 v = TA::get(raw, j);
-        u[j] = make_float4(v.x * keep, v.y * keep, v.z * keep, v.w * keep);
-      }
-      if (do_bias) {
-        float4 c = u[0];
-#pragma unroll
-        for (int j = 1; j < 8; ++j) c = f4add(c, u[j]);
-        bsum[0] += c.x;
-        bsum[1] += c.y;
-        bsum[2] += c.z;
-        bsum[3] += c.w;
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) u[j] = TB::get(raw, j);
-    }
-    if (act) {
-      const float f0[8] = {u[0].x, u[1].x, u[2].x, u[3].x, u[4].x, u[5].x, u[6].x, u[7].x};
-      const float f1[8] = {u[0].y, u[1].y, u[2].y, u[3].y, u[4].y, u[5].y, u[6].y, u[7].y};
-      const float f2[8] = {u[0].z, u[1].z, u[2].z, u[3].z, u[4].z, u[5].z, u[6].z, u[7].z};
-      const float f3[8] = {u[0].w, u[1].w, u[2].w, u[3].w, u[4].w, u[5].w, u[6].w, u[7].w};
-      put(img, 0, f0);
-      put(img, 1, f1);
-      put(img, 2, f2);
-      put(img, 3, f3);
-    }
-  };
-
-  floatx4 acc[RN > 0 ? RN : 1][TNK], accx[RX > 0 ? RX : 1];
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int j = 0; j < TNK; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int x = 0; x < RX; ++x) accx[x] = floatx4{0.f, 0.f, 0.f, 0.f};
-  // remainder product x of this wave: n-fragment RN WAVES + q / TNK, k-fragment q % TNK (q past
-  // the remainder computes clamped data, discarded)
-  auto xq = [&](int x) {
-    const int q = w + x * WAVES;
-    return q < S::REM ? q : 0;
-  };
-  auto compute = [&](int buf) {
-    const b3_u4* img = b3_lds + buf * SU4;
-    b3_u4 ah[RN > 0 ? RN : 1], al2[RN > 0 ? RN : 1];
-#pragma unroll
-    for (int i = 0; i < RN; ++i) {
-      const int row = (w + i * WAVES) * 16 + rrow;
-      ah[i] = img[row * 4 + sw];
-      al2[i] = img[(COLS + row) * 4 + sw];
-    }
-#pragma unroll
-    for (int x = 0; x < RX; ++x) {
-      const int q = xq(x);
-      const int ra = (RN * WAVES + q / TNK) * 16 + rrow, rb = AC + (q % TNK) * 16 + rrow;
-      const b3_u4 xah = img[ra * 4 + sw], xal = img[(COLS + ra) * 4 + sw];
-      const b3_u4 xbh = img[rb * 4 + sw], xbl = img[(COLS + rb) * 4 + sw];
-      floatx4 c = accx[x];
-      c = b3_mfma(xal, xbh, c);
-      c = b3_mfma(xah, xbl, c);
-      accx[x] = b3_mfma(xah, xbh, c);
-    }
-#pragma unroll
-    for (int j = 0; j < TNK; ++j) {
-      if constexpr (RN > 0) {
-        const int row = AC + j * 16 + rrow;
-        const b3_u4 bh = img[row * 4 + sw], bl_ = img[(COLS + row) * 4 + sw];
-#pragma unroll
-        for (int i = 0; i < RN; ++i) {
-          floatx4 c = acc[i][j];
-          c = b3_mfma(al2[i], bh, c);
-          c = b3_mfma(ah[i], bl_, c);
-          acc[i][j] = b3_mfma(ah[i], bh, c);
-        }
-      }
-    }
-  };
-
-  if (nt > 0) {
-    index(0);
-    address(0);
-    fetch();
-    index(1);
-    stage(0, 0);
-    address(1);
-    __syncthreads();
-    for (int t = 0; t < nt; ++t) {
-      index(t + 2);
-      fetch();  // step t + 1 (steps past the split read in-bounds rows, masked when staged)
-      __builtin_amdgcn_sched_barrier(0);  // keep the loads ahead of the MFMAs (no sinking)
-      compute(t & 1);
-      if (t + 1 < nt) stage(t + 1, (t + 1) & 1);
-      address(t + 2);
-      __syncthreads();
-    }
-  }
-
-  // ---- epilogue: accumulators straight to the slab (rows n = 16 nf + 4 fg + r, columns
-  // k0 + 16 j + fr: 64 contiguous bytes per row and register) ----
-  const int ldk = (Kout + 3) & ~3;
-  float* out = slab + (int64_t)split * Nout * ldk;
-  auto store = [&](int nf, int kf, const floatx4& c) {
-    const int col = k0 + kf * 16 + fr;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = nf * 16 + fg * 4 + r;
-      if (row < Nout && col < Kout) out[(int64_t)row * ldk + col] = c[r];
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int j = 0; j < TNK; ++j) store(w + i * WAVES, j, acc[i][j]);
-#pragma unroll
-  for (int x = 0; x < RX; ++x) {
-    const int q = w + x * WAVES;
-    if (q < S::REM) store(RN * WAVES + q / TNK, q % TNK, accx[x]);
-  }
-  if (do_bias) {
-    // column sums: an A stager holds columns jcol .. jcol + 3 of chunk jc
-    if (wa)
-#pragma unroll
-      for (int t4 = 0; t4 < 4; ++t4) bpart[jc * AC + jcol + t4] = bsum[t4];
-    __syncthreads();
-    for (int n = tid; n < Nout; n += NT)
-      bslab[(int64_t)split * Nout + n] =
-          (bpart[n] + bpart[AC + n]) + (bpart[2 * AC + n] + bpart[3 * AC + n]);
-  }
-}
-
-template <int TNN, int TNK, class AL, class BL>
-inline hipError_t launch_b3tn_t(const AL& al, const BL& bl, const B3TnPlan& p, float* slab,
-                                float* bslab, int Nout, int Kout, int R, bool want_bias,
-                                hipStream_t st) {
-  using S = B3TnShape<TNN, TNK>;
-  auto kern = gemm_b3tn_kernel<TNN, TNK, AL, BL>;
-  static LdsLimit lim;
-  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), 160 * 1024);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(p.tiles_k * p.splits), dim3(S::NT), S::LDS_BYTES, st, al, bl, slab,
-                     bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
-  return hipGetLastError();
-}
-
-constexpr int kB3TnTnk = 5;  // k fragments per workgroup (H = 400: 25 -> 5 tiles exactly)
+// k fragments per workgroup: 5 (H = 400: 25 -> 5 tiles exactly); 4 for more than 25 n-fragments
+// (H = 512: 32 -> 8 tiles), whose accumulators would not fit beside TNK = 5 (40 B of scratch)
+inline int b3tn_tnk(int Nout) { return (Nout + 15) / 16 > 25 ? 4 : 5; }
 // workgroups of the layer weight gradient (A/B in the step: 128 -0.8 %, 256 -1.1 % vs 176; the
 // side stream shares the GPU with the main chain, fewer splits = smaller slabs)
 constexpr int kB3TnTarget = 176;
 inline B3TnPlan b3tn_plan(int Nout, int Kout, int R, int target = kB3TnTarget) {
-  return plan_b3tn(Nout, Kout, R, kB3TnTnk, target);
+  return plan_b3tn(Nout, Kout, R, b3tn_tnk(Nout), target);
 }
-// the A side (Nout) is held whole per workgroup: supported n-fragment counts; operand extents
-// must fit the 32-bit element offsets
-template <class AL, class BL>
-inline bool b3tn_ok(const AL& al, const BL& bl, int Nout, int R) {
-  const int t = (Nout + 15) / 16;
-  // (t == 32, H = 512, compiles but runs 3.4x slower than the register-direct fp32 TN there:
-  //  633 vs 186 us per layer weight gradient at cfg5; those shapes take the fp32 kernels)
-  const bool shape = t == 25 || t == 8 || t == 3 || t == 2 || t == 6;
-  return shape && B3TnSrc<AL>::fits(al, R) && B3TnSrc<BL>::fits(bl, R);
-}
-// slab bytes the plan needs: splits x Nout x round4(Kout) floats (+ splits x Nout bias)
-template <class AL, class BL>
-inline hipError_t launch_b3tn(const AL& al, const BL& bl, const B3TnPlan& p, float* slab,
-                              float* bslab, int Nout, int Kout, int R, bool want_bias,
-                              hipStream_t st) {
-  constexpr int TNK = kB3TnTnk;
-  if (!b3tn_ok(al, bl, Nout, R)) return hipErrorInvalidValue;
-  switch (p.tnn) {
-    case 25: return launch_b3tn_t<25, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-    case 32: return launch_b3tn_t<32, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-    case 8: return launch_b3tn_t<8, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-    case 6: return launch_b3tn_t<6, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-    case 3: return launch_b3tn_t<3, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-    case 2: return launch_b3tn_t<2, TNK>(al, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-  }
-  return hipErrorInvalidValue;
-}
-
-
 // ------------------------------------------------------------------------------------------
 // TN with the n-side operand as a pre-split e-image (weight gradients dW = A^T B whose A is
 // shared by every k-tile: dpre, dzn, Gs)
@@ -928,9 +645,9 @@ inline hipError_t launch_b3tn(const AL& al, const BL& bl, const B3TnPlan& p, flo
 // holding the pieces of rows 32 s .. 32 s + 31 in order; rows >= R and columns >= C are zero.
 // Written once per matrix by b3_eimage (b3_pack.hip).  An MFMA A fragment (16 columns x 32 rows)
 // is then one coalesced 1 KB global load per piece: lane (fr, fg) takes column fr, rows
-// 8 fg .. 8 fg + 7 -- no transposition and no split inside the GEMM, where gemm_b3tn_kernel
-// re-staged and re-split the whole A operand in each of its tiles_k workgroups (5 at H = 400:
-// 83 % of its staging VALU, PMC 7.6 VALU per MFMA).
+// 8 fg .. 8 fg + 7 -- no transposition and no split inside the GEMM (the round-2 kernel re-staged
+// and re-split the whole A operand in each of its tiles_k workgroups, 5 at H = 400: 83 % of its
+// staging VALU, PMC 7.6 VALU per MFMA).
 struct B3EImg {
   const b3_u4* img;  // 16-byte units: ((s * 2 + p) * cimg + c) * 4 + chunk
   int cimg;          // columns, a multiple of 16
@@ -1260,11 +977,13 @@ template <class BL>
 inline hipError_t launch_b3tni(const B3EImg& ai, const BL& bl, const B3TnPlan& p, float* slab,
                                float* bslab, int Nout, int Kout, int R, bool want_bias,
                                hipStream_t st) {
-  constexpr int TNK = kB3TnTnk;
+  constexpr int TNK = 5;
   if (!b3tni_ok(bl, Nout, R) || p.rows_per_split % 32) return hipErrorInvalidValue;
+  if (p.tiles_k != (Kout + 16 * b3tn_tnk(Nout) - 1) / (16 * b3tn_tnk(Nout)))
+    return hipErrorInvalidValue;  // a plan from b3tn_plan
   switch (p.tnn) {
     case 25: return launch_b3tni_t<25, TNK>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-    case 32: return launch_b3tni_t<32, TNK>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+    case 32: return launch_b3tni_t<32, 4>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
     default: break;
   }
   // other widths: the smallest instantiated fragment count that covers Nout (extra fragments
@@ -1277,7 +996,7 @@ inline hipError_t launch_b3tni(const B3EImg& ai, const BL& bl, const B3TnPlan& p
   if (t <= 16) { q.tnn = 16; return launch_b3tni_t<16, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
   if (t <= 25) { q.tnn = 25; return launch_b3tni_t<25, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
   q.tnn = 32;
-  return launch_b3tni_t<32, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st);
+  return launch_b3tni_t<32, 4>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st);
 }
 
 }  // namespace cgr

@@ -81,17 +81,6 @@ static hipError_t b3tni_gemm(const char* name, const float* A, int64_t lda, void
   return b3tni_run(name, img, bl, Nout, Kout, R, slab, bslab, want_bias, plan, st, target);
 }
 
-// split-bf16 TN (gemm_b3.hpp); same slab layout as tn_gemm
-template <class AL, class BL>
-static hipError_t b3tn_gemm(const char* name, const AL& al, const BL& bl, int Nout, int Kout, int R,
-                            float* slab, float* bslab, bool want_bias, TnPlan* plan,
-                            hipStream_t st, int target = kB3TnTarget) {
-  const B3TnPlan q = b3tn_plan(Nout, Kout, R, target);
-  *plan = TnPlan{1, q.tiles_k, q.splits, q.rows_per_split};
-  ProfScope _p(name, st);
-  return launch_b3tn(al, bl, q, slab, bslab, Nout, Kout, R, want_bias, st);
-}
-
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
                             int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                             hipStream_t st, int gap_at = 0, int gap_len = 0, bool flat = false) {
@@ -138,7 +127,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
 
   // readout (the head's dwf / dbf sums run on the side stream below)
   {
-    ProfScope _p("head_readout_bwd", st);
+    ProfScope _p("readout_act_bwd", st);
     HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
                             Hp, d.act, dzn, st));
   }
@@ -147,7 +136,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   {
     HIP_RET(fork_to(ss, st, side));
     {  // dwf = dy^T g, dbf: off the main chain (step A/B +0.8 %)
-      ProfScope _p("head_readout_bwd", side);
+      ProfScope _p("head_bwd", side);
       HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
                        grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], side));
     }

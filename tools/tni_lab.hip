@@ -1,6 +1,6 @@
 // Lab for the e-image split-bf16 TN (csrc/gemm_b3.hpp gemm_b3tni_kernel): correctness against an
 // fp64 host reference and timing at the cfg2 shapes (layer, readout-like, node weight gradients).
-// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 [-DCGR_TNI_LAB=mask] tools/tni_lab.hip
+// Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -Iinclude [-DCGR_TNI_LAB=mask] tools/tni_lab.hip
 //   ablation mask: 1 no B loads, 2 no A loads, 4 no MFMA, 8 no B staging (split + LDS stores)
 #include <hip/hip_runtime.h>
 #include <math.h>

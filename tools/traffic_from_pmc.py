@@ -69,7 +69,7 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
         return "segsum_src_bwd" if "<true>" in n else "segsum_dst_fwd"
     table = {"k_edge_init_seg": "edge_init_seg_fwd", "k_edge_init": "edge_init_fwd",
              "k_layer_bwd": "layer_act_bwd", "k_pool_head": "pool_head_fwd",
-             "k_head_bwd": "head_readout_bwd", "k_readout_bwd": "head_readout_bwd",
+             "k_head_bwd": "head_bwd", "k_readout_bwd": "readout_act_bwd",
              "k_reduce_slabs": "splitk_reduce"}
     for k, v in table.items():
         if re.search(r"\b" + k + r"[<(]", n):
