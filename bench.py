@@ -107,13 +107,16 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
         f4 * (N * H + N * F + N * H + H * (F + H) + H))
     add("gemm_nt_readout_bwd", 1, 2.0 * N * H * H, f4 * (N * H + H * H + N * H))
     add("layer_act_bwd", 1, 0.0, f4 * (N * H + 2 * E * H) + i4 * E)  # top layer: dh = ds[dst]
-    # da = segsum_src(dm) fused with the layer below's activation backward (D - 1 launches: dm once,
-    # h_{l+1} mask, dpre write) or the edge-init backward (1: dm, h_0 mask, the D layers' dpre
-    # summed into dh0, dpre0 write); per launch on average 4 E*H floats (+ indices)
-    add("segsum_act_bwd", D, 2.0 * E * H, f4 * (4 * E * H) + i4 * (2 * E + 2 * (N + 1)))
     add("gemm_tn_wgrad_layer", D, 2.0 * E * H * H,
         f4 * (E * H + N * H + E * H + H * H + H) + 2 * i4 * E)
-    add("gemm_nt_layer_bwd", D, 2.0 * E * H * H, f4 * (E * H + H * H + E * H))
+    # dm = dpre_l W_l with da = segsum_src(dm) and the layer below's activation backward in its
+    # epilogue (D - 1 launches: dpre_l rows, W_l, the h mask, dpre_{l-1} written) or the edge-init
+    # backward (1: + the D layers' dpre summed into dh0): per launch on average 4 E*H + H*H floats
+    add("gemm_nt_layer_bwd_seg", D, 2.0 * E * H * H + E * H,
+        f4 * (4 * E * H + H * H) + i4 * (2 * E))
+    # its fixup: the dst segments crossing a 128-row tile (about one per tile, E/N rows each):
+    # the raw rows, their mask and the dpre rows written
+    add("bwd_seg_fixup", D, 0.0, f4 * (E / 128.0) * (E / max(N, 1)) * 3 * H + i4 * 2 * (E / 128.0))
     add("segsum_src_bwd", 1, E * H, seg_dst + i4 * E)  # Gs = segsum_src(dpre0) for dW0[:, :F]
     add("gemm_tn_wgrad_edge", 1, 2.0 * E * H * Fe, f4 * (E * H + E * Fe + H * Fe + H))
     add("gemm_tn_wgrad_node", 1, 2.0 * N * H * F, f4 * (N * H + N * F + H * F))
@@ -135,7 +138,7 @@ def mfma_bound(name):
 # weight gradients into two (three products); the edge-feature weight gradient (K = Fe = 14)
 # stays on the fp32 MFMA (v_mfma_f32_16x16x4_f32)
 BF16_PRODUCTS = {"gemm_nt_x": 6, "gemm_nt_layer_fwd": 6, "gemm_nt_layer_seg_fwd": 6,
-                 "gemm_nt_readout_fwd": 6, "gemm_nt_layer_bwd": 6, "gemm_nt_readout_bwd": 6,
+                 "gemm_nt_readout_fwd": 6, "gemm_nt_layer_bwd_seg": 6, "gemm_nt_readout_bwd": 6,
                  "gemm_tn_wgrad_layer": 3, "gemm_tn_wgrad_node": 3, "gemm_tn_wgrad_readout": 3}
 
 

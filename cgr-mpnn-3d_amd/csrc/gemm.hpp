@@ -106,6 +106,31 @@ struct LdPlain {
   }
 };
 
+// rows gathered through an index: A(r, :) = base[idx[r], :]  (internal buffers, ld % 4 == 0).
+// The layer backward's dm GEMM reads dpre[rev(r)] so that its output row r is dm[rev(r)]: rows
+// grouped by dst(r), the segments its fused epilogue sums (ep_bwd.hpp).
+struct LdGatherRows {
+  const float* base;
+  const int* idx;
+  int64_t ld;
+  struct Row {
+    int i;
+    bool ok;
+  };
+  typedef float4 Raw;
+  __device__ __forceinline__ Row row(int r, int limit) const {
+    const bool ok = r < limit;
+    return Row{idx[ok ? r : 0], ok};
+  }
+  __device__ __forceinline__ Raw fetch(const Row& rw, int k, int K) const {
+    return *reinterpret_cast<const float4*>(base + (int64_t)rw.i * ld + (k < K ? k : 0));
+  }
+  __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
+    return mask4(v, rw.ok, k, K);
+  }
+  __device__ __forceinline__ float4 combine_nm(const Raw& v) const { return v; }
+};
+
 // B rows of two stacked weight matrices: rows [0, n0) from base0 (ld0), rows [n0, ...) from base1
 // (ld1).  Used for the merged x-GEMM  x @ [W0[:, :F]; W_n[:, :F]]^T.  VEC divides ld0, ld1, K.
 template <int VEC>

@@ -167,6 +167,12 @@ inline B3PackJob b3_job(const float* src, int64_t ldn, int64_t ldk, int N, int K
 // ------------------------------------------------------------------------------------------
 // NT kernel
 // ------------------------------------------------------------------------------------------
+// epilogue functors with kTile = true take the whole accumulator tile (EpLayerBwdSeg)
+template <class EP, class = void>
+struct b3_ep_tile : std::false_type {};
+template <class EP>
+struct b3_ep_tile<EP, std::void_t<decltype(EP::kTile)>> : std::bool_constant<EP::kTile> {};
+
 template <int WAVES, int RF, int NF>
 struct B3NtShape {
   static constexpr int NT = WAVES * 64;
@@ -175,7 +181,9 @@ struct B3NtShape {
   static constexpr int BPT = (BU4 + NT - 1) / NT;
   static constexpr int LDC = BN + 4;
   static constexpr size_t STAGE_BYTES = 3 * BU4 * 16;
-  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4;  // + EpLayerSeg's dst
+  // + the dst of rows m0 - 1 .. m0 + BM (EpLayerSeg, EpLayerBwdSeg) and 16 floats of reduction
+  // scratch (EpLayerBwdSeg; kernels with static LDS cannot be given the full 160 KB dynamically)
+  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4 + 64;
   static constexpr size_t LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
 };
 
@@ -402,8 +410,10 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   }
   float* C = reinterpret_cast<float*>(b3_lds);
   constexpr bool SEG = EP::kSeg;  // the epilogue also sums the tile's dst segments (EpLayerSeg)
-  int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG: dst of rows m0 - 1 .. m0 + BM
-  if constexpr (SEG) {
+  // the whole tile goes to the functor (EpLayerBwdSeg: ep_bwd.hpp)
+  constexpr bool TILE = b3_ep_tile<EP>::value;
+  int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG / TILE: dst of rows m0 - 1 .. m0 + BM
+  if constexpr (SEG || TILE) {
     for (int q = tid; q < BM + 2; q += NT) {
       const int r = m0 - 1 + q;
       sd[q] = (r >= 0 && r < M) ? ep.dst_s[r] : -1 - (r >= M);  // distinct sentinels
@@ -417,6 +427,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       for (int r = 0; r < 4; ++r)
         C[((w * RF + i) * 16 + fg * 4 + r) * S::LDC + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
+  if constexpr (TILE) {
+    ep.template tile<BM, BN, NT, S::LDC, EIT>(pv, C, sd, m0, n0, tile, tid);
+  } else {
 #pragma unroll
   for (int it = 0; it < EIT; ++it) {
     const int q = tid + it * NT;
@@ -470,6 +483,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       }
     }
   }
+  }  // !TILE
 }
 
 template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP>

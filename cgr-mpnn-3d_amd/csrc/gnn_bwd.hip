@@ -1,7 +1,8 @@
 // Reverse mode of gnn_fwd.hip (the math is restated and pinned in
 // oracle/dmpnn_numpy.py::backward).  Same gather -> MFMA GEMM -> segmented-reduce pattern as the
 // forward with src and dst swapped; weight gradients are split-K TN GEMMs over the edge / node
-// dimension reduced deterministically; no atomics anywhere, so gradients are bitwise stable.
+// dimension reduced deterministically; the only atomics add the two partial sums of a segment
+// that crosses a row tile onto zero (order-independent), so gradients are bitwise stable.
 //
 //   dwf = dy^T g ; dbf = sum dy ; dzn = dy[graph(v)] wf * act'(zn)        (ffn, pool, edge_to_node)
 //   dW_n = dzn^T [x | s], db_n = colsum(dzn), ds = dzn W_n[:, F:]
@@ -9,17 +10,20 @@
 //   for l = D-1 .. 0:
 //     dpre_l = dh_{l+1} * mask * act'(pre_l) ; ds_l = sum dpre_l*h0
 //     dW_l = dpre^T (a_l[src] - h_l[rev])  (message recomputed, never stored) ; db_l = colsum
-//     dm = dpre W_l ; da = segsum_src(dm) ; dh_l = da[dst] - dm[rev]  (one fused kernel with the
-//     next lower layer's dpre, da never stored: k_segsum_act_bwd)
+//     dm = dpre W_l ; da = segsum_src(dm) ; dh_l = da[dst] - dm[rev] -> the next lower layer's
+//     dpre, all in the dm GEMM's epilogue (EpLayerBwdSeg, ep_bwd.hpp: rows gathered through rev
+//     so each dst segment's rows are the dm rows its node sums; dm and da never stored) plus a
+//     small fixup launch for the segments that cross a row tile (bwd_seg_fixup)
 //   dh0 = sum_l s_l dpre_l (every layer's skip term) ; dpre0 = (dh0 + dh_0) * act'(pre0)
 //   dW0[:, F:] = dpre0^T e ; db0 = colsum(dpre0) ; dW0[:, :F] = (segsum_src dpre0)^T x
 //
-// Streams: the critical path is act_bwd -> dm GEMM -> segsum per layer.  Every weight-gradient
-// TN GEMM (+ its slab reduction) only feeds the gradient outputs, so it runs on the side stream,
+// Streams: the critical path is act_bwd -> (dm GEMM + fused epilogue -> fixup) per layer.
+// Every weight-gradient TN GEMM (+ its slab reduction) only feeds the gradient outputs, so it runs on the side stream,
 // forked right after its input is produced; every layer's dpre has a buffer of its own (the
 // edge-init backward sums them into dh0), so the main stream waits for the side stream only at
 // the very end.
 #include "dispatch.hpp"
+#include "ep_bwd.hpp"
 #include "epilogues.hpp"
 #include "gnn_internal.hpp"
 #include "kernels.hpp"
@@ -110,6 +114,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   float* dsig_part = reinterpret_cast<float*>(ws + WL.dsig_part);
   void* img_side = ws + WL.img_side;
   void* img_main = ws + WL.img_main;
+  // partial sums of tile-crossing segments, accumulated by layer l's fused backward GEMM: two
+  // buffers, alternating by layer (each fixup zeroes the next layer's)
+  auto dag_of = [&](int l) {
+    return reinterpret_cast<float*>(ws + WL.dag) + (l & 1) * (int64_t)d.N * d.Hp;
+  };
 
   const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
   // dpre of layer l: a buffer per layer, so that writing dpre_{l-1} never waits for the side
@@ -189,8 +198,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
                         EpStore{ds, Hp, N, H, nullptr}, N, H, H, st));
   }
 
-  // learnable-skip partial-sum slots per layer (same count for the fused and unfused kernels)
-  const int nb = segsum_act_bwd_blocks(E, N, Hp);
+  // learnable-skip partial-sum slots per layer (bwd_dsig_slots)
+  const int nb = WL.dsig_blocks;
+  // row tile of the fused layer-backward GEMMs: crossing segments accumulate in dag
+  const int seg_rows = b3nt_rows(E, H);
+  const int seg_tiles = (int)cdiv(E, seg_rows) * b3_cols(H).tiles;
   auto layer_args = [&](int l) {
     uint32_t thresh;
     float scale;
@@ -218,8 +230,29 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   };
   if (D > 0) {  // top layer: dh_D = ds[dst]
     ProfScope _p("layer_act_bwd", st);
-    HIP_RET(layer_act_bwd(layer_args(D - 1), nb, st));
+    LayerBwdArgs la = layer_args(D - 1);
+    la.dag = dag_of(D - 1);
+    la.tile_rows = seg_rows;
+    HIP_RET(layer_act_bwd(la, nb, st));
   }
+  auto edge_args = [&]() {
+    LayerBwdArgs le{};
+    le.dm = dm;
+    le.rev_s = iv.rev_s;
+    le.h0 = fv.h[0];
+    le.pre = fv.pre[0];
+    le.act = d.act;
+    le.E = E;
+    le.H = H;
+    le.Hp = Hp;
+    le.dh0 = dh0;
+    le.dpre = dh0;  // dpre0 is written in place of dh0 (the buffer it names)
+    le.dpre_all = dpre(0);
+    le.dpre_stride = (int64_t)E * Hp;
+    le.nlayers = D;
+    for (int k = 0; k < D; ++k) le.sig[k] = d.learnable_skip ? params[CGR_PARAM_SKIP(D, k)] : nullptr;
+    return le;
+  };
   // edge init: dpre0 = (dh0 + dh_0) * act'(pre0), dh0 summed from the layers' dpre buffers,
   // written to the dh0 buffer
   float* dpre0 = dh0;
@@ -230,10 +263,20 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     // hardware queue (A/B 1.283 -> 1.263 ms; DESIGN.md §9 "Stream order")
     hipEvent_t fork_ev = nullptr;
     if (side != st) HIP_RET(record_point(ss, st, &fork_ev));
+    // dm = dpre_l W_l with the layer below's activation backward (or the edge init's) in the
+    // epilogue: rows gathered through rev, dst segments summed in the tile (ep_bwd.hpp)
+    const LayerBwdArgs lb = l > 0 ? layer_args(l - 1) : edge_args();
     {
-      ProfScope _p("gemm_nt_layer_bwd", st);
-      HIP_RET(launch_b3nt(LdPlain<4>{dp, Hp}, static_cast<const b3_u4*>(fv.b3lb[l]),
-                          EpStore{dm, Hp, E, H, nullptr}, E, H, H, st));
+      ProfScope _p("gemm_nt_layer_bwd_seg", st);
+      const LdGatherRows al{dp, iv.rev_s, Hp};
+      const b3_u4* img = static_cast<const b3_u4*>(fv.b3lb[l]);
+      float* dg = dag_of(l);
+      if (l > 0)
+        HIP_RET(launch_b3nt(al, img, EpLayerBwdSeg<false>{lb, dm, iv.dst_s, dg, iv.status, E, H},
+                            E, H, H, st));
+      else
+        HIP_RET(launch_b3nt(al, img, EpLayerBwdSeg<true>{lb, dm, iv.dst_s, dg, iv.status, E, H},
+                            E, H, H, st));
     }
     if (fork_ev) HIP_RET(hipStreamWaitEvent(side, fork_ev, 0));
     {  // side: dW_l = dpre^T m_l, db_l = colsum(dpre)
@@ -259,30 +302,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
                         grads[CGR_PARAM_CONV_B(l)], side));
       if (bucket_events) HIP_RET(hipEventRecord(bucket_events[D - l], side));
     }
-    // main: da[v] = sum_{src(e) = v} dm[e], consumed in place by the layer below:
-    // dh_l = da[dst] - dm[rev] -> dpre_{l-1} (or dpre0 of the edge init when l == 0)
-    ProfScope _p("segsum_act_bwd", st);
-    if (l > 0) {
-      HIP_RET(segsum_act_bwd(layer_args(l - 1), iv.src_list, iv.src_ptr, iv.dst_ptr, N, false,
-                             iv.status, st));
-    } else {
-      LayerBwdArgs le{};
-      le.dm = dm;
-      le.rev_s = iv.rev_s;
-      le.h0 = fv.h[0];
-      le.pre = fv.pre[0];
-      le.act = d.act;
-      le.E = E;
-      le.H = H;
-      le.Hp = Hp;
-      le.dh0 = dh0;
-      le.dpre = dpre0;
-      le.dpre_all = dpre(0);
-      le.dpre_stride = (int64_t)E * Hp;
-      le.nlayers = D;
-      for (int k = 0; k < D; ++k) le.sig[k] = d.learnable_skip ? params[CGR_PARAM_SKIP(D, k)] : nullptr;
-      HIP_RET(segsum_act_bwd(le, iv.src_list, iv.src_ptr, iv.dst_ptr, N, true, iv.status, st));
-    }
+    // main: the rows of tile-crossing dst segments (paired edges) or every row (unpaired)
+    ProfScope _p("bwd_seg_fixup", st);
+    HIP_RET(bwd_seg_fixup(lb, l == 0, iv.dst_s, iv.dst_ptr, iv.src_list, iv.src_ptr, dag_of(l),
+                          l > 0 ? dag_of(l - 1) : nullptr, iv.status, N, seg_rows, seg_tiles, nb,
+                          st));
   }
   float* gW0 = grads[CGR_PARAM_EDGE_INIT_W];
   float* gb0 = grads[CGR_PARAM_EDGE_INIT_B];

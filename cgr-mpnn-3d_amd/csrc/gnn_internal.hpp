@@ -104,10 +104,9 @@ struct ArenaLayout {
   size_t b3x, b3rof, b3rob, b3lf[CGR_MAX_DEPTH], b3lb[CGR_MAX_DEPTH];
 };
 
-// dpre of layer l lives in buffer l & 1 (a two-buffer ring): the layer-l+1 weight gradient must
-// finish reading before the fused src sum of layer l overwrites it -- one side->main wait per
-// layer (one buffer per layer, no wait: A/B 1.28 -> 1.35 ms, the graph then maps the freed
-// main-stream nodes onto the side stream's queue)
+// Backward workspace.  dpre has one buffer per layer (no side->main wait before a buffer is
+// rewritten; the edge-init backward sums dh0 from all of them); dm holds only the rows the fused
+// layer-backward GEMM leaves to its fixup (ep_bwd.hpp).
 struct WorkspaceLayout {
   size_t bytes;
   size_t dpre, dm, dh0, dzn, ds, Gs, slab, bslab, slab2, bslab2, dsig_part, slab_elems,
@@ -115,8 +114,12 @@ struct WorkspaceLayout {
   // split-bf16 e-images (gemm_b3.hpp B3EImg) of the weight gradients' shared operand: dpre_l and
   // dzn on the side stream (one at a time), Gs on the caller's stream
   size_t img_side, img_main;
+  // 2 x [N, Hp] partial da sums of the dst segments that cross a row tile of the fused
+  // layer-backward GEMM (ep_bwd.hpp), alternating by layer
+  size_t dag;
   int dsig_blocks;
 };
+int bwd_dsig_slots(const Dims& d);
 
 // Forward variants.  Training (cgr_gnn_forward): every activation the backward reads is saved in
 // the arena and the weight images are packed into it by each call.  Eval (cgr_gnn_predict): no

@@ -5,6 +5,7 @@
 // segment are contiguous (dst-sorted edges) so every wave reads whole 1.6 KB rows.
 #include "common.hpp"
 #include "kernels.hpp"
+#include "bwd_rows.hpp"
 
 namespace cgr {
 
@@ -485,9 +486,18 @@ __global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
   if (t < a.E * C4) {
     const int64_t i = t / C4;
     const int n = 4 * (int)(t - i * C4);
-    // top layer: dh_D[i] = ds[dst(i)] (lower layers: k_segsum_act_bwd)
+    // top layer: dh_D[i] = ds[dst(i)] (lower layers: the fused dm GEMM, ep_bwd.hpp)
     const float4 dh = *reinterpret_cast<const float4*>(a.ds + (int64_t)a.dst_s[i] * a.Hp + n);
     layer_bwd_row(a, i, n, dh, a.thresh ? *a.seed : 0, dsig);
+  }
+  if (a.dag) {  // zero what the fused layer-backward GEMMs accumulate (see EpLayerBwdSeg)
+    const int64_t nb = cdiv(a.E, a.tile_rows) - 1;  // interior row-tile boundaries
+    if (t < nb * C4) {
+      const int64_t m = (t / C4 + 1) * a.tile_rows;
+      const int n = 4 * (int)(t % C4);
+      const int v = a.dst_s[m];
+      if (a.dst_s[m - 1] == v) *reinterpret_cast<float4*>(a.dag + (int64_t)v * a.Hp + n) = f4zero();
+    }
   }
   if (a.dsig_part) block_partial(dsig, a.dsig_part);
 }
@@ -500,199 +510,90 @@ hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Operands of one float4 of one edge row of the layer / edge-init backward, loaded ahead of the
-// row's dh (so a node's rows issue all their loads together); *_apply is bitwise layer_bwd_row /
-// edge_init_bwd_row given the same values.
-struct RowOps {
-  float4 m;    // h_{l+1} (ReLU mask) or pre (other activations); edge init: h_0 or pre_0
-  float4 acc;  // edge init: dh0 = sum_l sigma_l dpre_l
-  float4 h0;   // h_0 (learnable-skip partials)
-};
-
-__device__ __forceinline__ RowOps layer_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
-  const int64_t o = i * a.Hp + n;
-  RowOps r;
-  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.hnext : a.pre) + o);
-  r.acc = f4zero();
-  r.h0 = a.dsig_part ? *reinterpret_cast<const float4*>(a.h0 + o) : f4zero();
-  return r;
-}
-
-__device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
-                                                uint64_t key, float& dsig, const RowOps& r) {
-  const int64_t o = i * a.Hp + n;
-  float d[4] = {dh.x, dh.y, dh.z, dh.w};
-  if (a.act == ACT_RELU) {
-    const float hh[4] = {r.m.x, r.m.y, r.m.z, r.m.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
-  } else {
-    const float zz[4] = {r.m.x, r.m.y, r.m.z, r.m.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float m = a.scale;
-      if (a.thresh && n + k < a.H)
-        m = drop_keep(key, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
-                                                                                      : 0.f;
-      d[k] = d[k] * m * act_grad(zz[k], a.act);
-    }
-  }
-  const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
-  *reinterpret_cast<float4*>(a.dpre + o) = dp;
-  if (a.dsig_part) {
-    const float hz[4] = {r.h0.x, r.h0.y, r.h0.z, r.h0.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (n + k < a.H) dsig += d[k] * hz[k];
-  }
-}
-
-// dh0 = sum_l sigma_l dpre_l (GNN.py:97: every layer adds sigma_l h0), summed from the top layer
-// down, one sigma-weighted float4 per layer buffer
-__device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
-  const int64_t o = i * a.Hp + n;
-  RowOps r;
-  r.m = *reinterpret_cast<const float4*>((a.act == ACT_RELU ? a.h0 : a.pre) + o);
-  float4 acc = f4zero();
-  for (int l = a.nlayers - 1; l >= 0; --l) {
-    const float sg = a.sig[l] ? a.sig[l][0] : 1.f;
-    const float4 dp = *reinterpret_cast<const float4*>(a.dpre_all + l * a.dpre_stride + o);
-    acc.x += sg * dp.x;
-    acc.y += sg * dp.y;
-    acc.z += sg * dp.z;
-    acc.w += sg * dp.w;
-  }
-  r.acc = acc;
-  r.h0 = f4zero();
-  return r;
-}
-
-__device__ __forceinline__ void edge_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
-                                               const RowOps& r) {
-  const int64_t o = i * a.Hp + n;
-  float4 d = f4add(r.acc, dh);
-  if (a.act == ACT_RELU) {
-    d.x = r.m.x > 0.f ? d.x : 0.f;
-    d.y = r.m.y > 0.f ? d.y : 0.f;
-    d.z = r.m.z > 0.f ? d.z : 0.f;
-    d.w = r.m.w > 0.f ? d.w : 0.f;
-  } else {
-    d.x *= act_grad(r.m.x, a.act);
-    d.y *= act_grad(r.m.y, a.act);
-    d.z *= act_grad(r.m.z, a.act);
-    d.w *= act_grad(r.m.w, a.act);
-  }
-  *reinterpret_cast<float4*>(a.dpre + o) = d;
-}
-
-// src segmented sum of dm fused with the consumer of its result (the next lower layer's
-// activation backward, or the edge-init backward).  Thread (v, float4 column c):
-//   da[v] = sum_{src(e) = v} dm[e]
-//   for every edge i with dst(i) = v (contiguous in dst order):  dh = da[v] - dm[rev(i)], then
-//   the layer / edge-init backward of row i.
-// Paired edges (graph prep's status bit 2 clear: src(e ^ 1) == dst(e) for every e, the CGR edge
-// order of graph_features.py:184-195) make {rev(i) : dst(i) = v} exactly {e : src(e) = v}: the
-// rows summed into da ARE the rows each incoming edge subtracts, so every dm row is loaded once
-// (in the order of v's incoming edges, four at a time with clamped indices, no branches), kept in
-// registers for the node's first four edges, and the rows' operands are loaded beside them.
-// Unpaired edge lists (any other edge_index) take the src-CSR gather.  da never reaches memory.
-// The grid is a.nblocks blocks (>= the threads needed) so the learnable-skip partial sums fill
-// exactly the slots the unfused kernel fills.
+// Completion of the fused layer-backward GEMM (ep_bwd.hpp), grid-stride.  Paired: thread =
+// (interior row-tile boundary m, row slot k < kFixupRows, float4 column); the segment of
+// v = dst(m) crosses the boundary when dst(m - 1) == v and is completed at the first boundary it
+// crosses: da = dag[v] (both partials in), dh = da - dm[rev(i)] for rows i = ib + k, ib + k + 4 ..
+// of the segment (a.dm holds those rows raw); the slot-0 thread zeroes v's entry of the NEXT
+// layer's partial-sum buffer (dag_next: the two alternate, so no thread reads what another
+// zeroes).  Unpaired: thread = (node, float4 column), the src segmented sum da[v] over
+// the raw rows (row r of a.dm is dm[rev(r)], so dm[e] = a.dm[rev(e)]).
+constexpr int kFixupRows = 4;
 template <bool EDGE_INIT>
-__global__ __launch_bounds__(256) void k_segsum_act_bwd(LayerBwdArgs a, const int* __restrict__ src_list,
-                                                        const int* __restrict__ src_ptr,
-                                                        const int* __restrict__ dst_ptr, int64_t N,
-                                                        const int* __restrict__ status) {
+__global__ __launch_bounds__(256) void k_bwd_seg_fixup(LayerBwdArgs a, const int* __restrict__ dst_s,
+                                                       const int* __restrict__ dst_ptr,
+                                                       const int* __restrict__ src_list,
+                                                       const int* __restrict__ src_ptr,
+                                                       const float* __restrict__ dag,
+                                                       float* __restrict__ dag_next,
+                                                       const int* __restrict__ status, int64_t N,
+                                                       int tile_rows, int slot0, int nslots) {
   const int C4 = a.Hp >> 2;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float dsig = 0.f;
   const bool paired = (*status & 4) == 0;
-  if (t < N * C4) {
-    const int64_t v = t / C4;
-    const int n = 4 * (int)(t - v * C4);
-    const float* base = a.dm + n;
-    auto ld4 = [&](int64_t r) { return *reinterpret_cast<const float4*>(base + r * a.Hp); };
-    auto loads = [&](int64_t i) {
-      if constexpr (EDGE_INIT) return edge_row_loads(a, i, n);
-      else return layer_row_loads(a, i, n);
-    };
-    const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
-    auto apply = [&](int64_t i, float4 dh, const RowOps& r) {
-      if constexpr (EDGE_INIT) edge_row_apply(a, i, n, dh, r);
-      else layer_row_apply(a, i, n, dh, key, dsig, r);
-    };
-    const int ib = dst_ptr[v], ie = dst_ptr[v + 1];
-    if (paired) {
-      const int deg = ie - ib;
+  const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float dsig = 0.f;
+  auto ld4 = [&](int64_t r, int n) {
+    return *reinterpret_cast<const float4*>(a.dm + r * a.Hp + n);
+  };
+  if (paired) {
+    const int64_t nb = cdiv(a.E, tile_rows) - 1;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nb * kFixupRows * C4;
+         t += stride) {
+      const int64_t bk = t / C4;
+      const int n = 4 * (int)(t - bk * C4);
+      const int64_t m = (bk / kFixupRows + 1) * tile_rows;
+      const int k = (int)(bk % kFixupRows);
+      const int v = dst_s[m];
+      if (dst_s[m - 1] != v) continue;
+      const int ib = dst_ptr[v], ie = dst_ptr[v + 1];
+      if (ib < m - tile_rows) continue;  // crossed an earlier boundary: completed there
+      const int64_t o = (int64_t)v * a.Hp + n;
+      const float4 da = *reinterpret_cast<const float4*>(dag + o);
+      if (k == 0 && dag_next) *reinterpret_cast<float4*>(dag_next + o) = f4zero();
+      for (int i = ib + k; i < ie; i += kFixupRows)
+        bwd_row_apply<EDGE_INIT>(a, i, n, f4sub(da, ld4(i, n)), key, dsig,
+                                 bwd_row_loads<EDGE_INIT>(a, i, n));
+    }
+  } else {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < N * C4; t += stride) {
+      const int64_t v = t / C4;
+      const int n = 4 * (int)(t - v * C4);
       float4 da = f4zero();
-      float4 r[4];
-      RowOps ops[4];
-      if (deg > 0) {
-        int ri[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ri[k] = a.rev_s[min(ib + k, ie - 1)];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) r[k] = ld4(ri[k]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ops[k] = loads(min(ib + k, ie - 1));
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (k < deg) da = f4add(da, r[k]);
-        for (int c = 4; c < deg; c += 4) {  // high-degree nodes: the rest of the sum
-          float4 x[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) x[k] = ld4(a.rev_s[min(ib + c + k, ie - 1)]);
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (c + k < deg) da = f4add(da, x[k]);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          if (k < deg) apply(ib + k, f4sub(da, r[k]), ops[k]);
-        for (int i = ib + 4; i < ie; ++i) apply(i, f4sub(da, ld4(a.rev_s[i])), loads(i));
-      }
-    } else {
-      const int b = src_ptr[v], e = src_ptr[v + 1];
-      float4 da = f4zero();
-      int j = b;
-      for (; j + 4 <= e; j += 4) {
-        const int64_t r0 = src_list[j], r1 = src_list[j + 1], r2 = src_list[j + 2],
-                      r3 = src_list[j + 3];
-        const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2), x3 = ld4(r3);
-        da = f4add(f4add(f4add(f4add(da, x0), x1), x2), x3);
-      }
-      const int rem = e - j;
-      if (rem > 0) {
-        const int64_t r0 = src_list[j], r1 = src_list[min(j + 1, e - 1)],
-                      r2 = src_list[min(j + 2, e - 1)];
-        const float4 x0 = ld4(r0), x1 = ld4(r1), x2 = ld4(r2);
-        da = f4add(da, x0);
-        if (rem > 1) da = f4add(da, x1);
-        if (rem > 2) da = f4add(da, x2);
-      }
-      for (int i = ib; i < ie; ++i) apply(i, f4sub(da, ld4(a.rev_s[i])), loads(i));
+      for (int j = src_ptr[v], e = src_ptr[v + 1]; j < e; ++j)
+        da = f4add(da, ld4(a.rev_s[src_list[j]], n));
+      for (int i = dst_ptr[v], e = dst_ptr[v + 1]; i < e; ++i)
+        bwd_row_apply<EDGE_INIT>(a, i, n, f4sub(da, ld4(i, n)), key, dsig,
+                                 bwd_row_loads<EDGE_INIT>(a, i, n));
     }
   }
-  if (!EDGE_INIT && a.dsig_part) block_partial(dsig, a.dsig_part);
+  if (!EDGE_INIT && a.dsig_part) {
+    block_partial(dsig, a.dsig_part + slot0);
+    for (int64_t s = slot0 + gridDim.x + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+         s < nslots; s += stride)
+      a.dsig_part[s] = 0.f;
+  }
 }
 
-int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp) {
-  return (int)cdiv((E > N ? E : N) * (Hp / 4), 256);
+int bwd_seg_fixup_blocks(int64_t E, int Hp, int tile_rows) {
+  const int64_t t = (cdiv(E, tile_rows) - 1) * kFixupRows * (Hp / 4);
+  const int64_t b = cdiv(t, 256);
+  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
 }
 
-hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int* src_ptr,
-                          const int* dst_ptr, int64_t N, bool edge_init, const int* status,
-                          hipStream_t st) {
-  if (N <= 0 || a.Hp % 4) return N <= 0 ? hipSuccess : hipErrorInvalidValue;
-  // as many blocks as the unfused layer kernel when learnable-skip partials are written
-  const int nb = (!edge_init && a.dsig_part) ? segsum_act_bwd_blocks(a.E, N, a.Hp)
-                                             : (int)cdiv(N * (a.Hp / 4), 256);
+hipError_t bwd_seg_fixup(const LayerBwdArgs& a, bool edge_init, const int* dst_s,
+                         const int* dst_ptr, const int* src_list, const int* src_ptr,
+                         const float* dag, float* dag_next, const int* status, int64_t N,
+                         int tile_rows, int slot0, int nslots, hipStream_t st) {
+  if (N <= 0 || a.E <= 0) return hipSuccess;
+  if (a.Hp % 4 || tile_rows <= 0) return hipErrorInvalidValue;
+  const int nb = bwd_seg_fixup_blocks(a.E, a.Hp, tile_rows);
   if (edge_init)
-    hipLaunchKernelGGL(k_segsum_act_bwd<true>, dim3(nb), dim3(256), 0, st, a, src_list, src_ptr,
-                       dst_ptr, N, status);
+    hipLaunchKernelGGL(k_bwd_seg_fixup<true>, dim3(nb), dim3(256), 0, st, a, dst_s, dst_ptr,
+                       src_list, src_ptr, dag, dag_next, status, N, tile_rows, slot0, nslots);
   else
-    hipLaunchKernelGGL(k_segsum_act_bwd<false>, dim3(nb), dim3(256), 0, st, a, src_list,
-                       src_ptr, dst_ptr, N, status);
+    hipLaunchKernelGGL(k_bwd_seg_fixup<false>, dim3(nb), dim3(256), 0, st, a, dst_s, dst_ptr,
+                       src_list, src_ptr, dag, dag_next, status, N, tile_rows, slot0, nslots);
   return hipGetLastError();
 }
 

@@ -59,8 +59,8 @@ hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_gra
                            float* dzn, hipStream_t st);
 
 struct LayerBwdArgs {
-  // dh_{l+1}: top layer (l == D-1, layer_act_bwd): ds[dst_s[i]]; below (segsum_act_bwd):
-  // da[dst(i)] - dm[rev_s[i]] with da = segsum_src(dm) computed in the same kernel
+  // dh_{l+1}: top layer (l == D-1, layer_act_bwd): ds[dst_s[i]]; below (the fused dm GEMM,
+  // ep_bwd.hpp, and its fixup): da[dst(i)] - dm[rev_s[i]], da = segsum_src(dm)
   const float* ds;
   const float* dm;
   const int* dst_s;
@@ -85,19 +85,24 @@ struct LayerBwdArgs {
   int64_t dpre_stride;
   int nlayers;
   const float* sig[CGR_MAX_DEPTH];
+  // top layer (layer_act_bwd): the entries of dag the fused layer-backward GEMMs accumulate
+  // (nodes whose dst segment crosses a tile_rows row-tile boundary) are zeroed (nullable)
+  float* dag;
+  int tile_rows;
 };
 // nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
 hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);
 int layer_act_bwd_blocks(int64_t E, int Hp);
-// da = segsum_src(dm) (never stored) fused with the layer backward of every edge row i whose
-// dst is the segment's node (dh = da[dst(i)] - dm[rev(i)]), or with the edge-init backward
-// (edge_init: dh0 from the layers' dpre buffers -> a.dpre, a.h0 / a.pre = h_0 / pre_0).  With learnable-skip
-// partials it launches segsum_act_bwd_blocks(E, N, Hp) blocks (size dsig_part accordingly).
-// status: graph prep's status word (bit 2 clear: paired edges, the fast form; see kernels.hip)
-hipError_t segsum_act_bwd(const LayerBwdArgs& a, const int* src_list, const int* src_ptr,
-                          const int* dst_ptr, int64_t N, bool edge_init, const int* status,
-                          hipStream_t st);
-int segsum_act_bwd_blocks(int64_t E, int64_t N, int Hp);
+// Completion of the fused layer-backward GEMM (EpLayerBwdSeg, ep_bwd.hpp; same LayerBwdArgs `a`,
+// a.dm = the raw rows it stored).  Paired edges: the rows of every dst segment that crosses a
+// tile_rows boundary (da = dag[v]; the same entries of dag_next, the buffer the next layer's GEMM
+// accumulates into, are zeroed); unpaired: every node in the src-CSR form.  Learnable-skip
+// partials: one per block at a.dsig_part[slot0 + block], slots up to nslots zero-filled.
+hipError_t bwd_seg_fixup(const LayerBwdArgs& a, bool edge_init, const int* dst_s,
+                         const int* dst_ptr, const int* src_list, const int* src_ptr,
+                         const float* dag, float* dag_next, const int* status, int64_t N,
+                         int tile_rows, int slot0, int nslots, hipStream_t st);
+int bwd_seg_fixup_blocks(int64_t E, int Hp, int tile_rows);
 
 // dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
 // gap_len > 0: slab columns [gap_at, gap_at + gap_len) are padding and skipped; later columns

@@ -33,6 +33,8 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
             return "gemm_tn_wgrad_readout"
         return "gemm_tn_wgrad_node"
     if "gemm_b3nt_kernel" in n:  # split-bf16 NT
+        if "EpLayerBwdSeg" in n:
+            return "gemm_nt_layer_bwd_seg"
         if "EpLayerSeg" in n:
             return "gemm_nt_layer_seg_fwd"
         if "EpLayer" in n:
@@ -41,8 +43,8 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
             return "gemm_nt_x"
         if "EpReadout" in n:
             return "gemm_nt_readout_fwd"
-        if "EpStore" in n:  # E-row layer GEMM on 8-wave tiles, N-row readout on 4-wave tiles
-            return "gemm_nt_readout_bwd" if "gemm_b3nt_kernel<4," in n else "gemm_nt_layer_bwd"
+        if "EpStore" in n:  # the readout backward (ds = dzn W_n[:, F:])
+            return "gemm_nt_readout_bwd"
     if "k_b3_eimage" in n:
         return "eimage"
     if "k_b3_pack" in n:
@@ -63,8 +65,8 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
         if m and m.group(1) != "4":
             return "gemm_tn_wgrad_node"
         return "gemm_tn_wgrad_edge"  # ambiguous only when F % 4 == 0; see note in the output
-    if "k_segsum_act_bwd" in n:
-        return "segsum_act_bwd"
+    if "k_bwd_seg_fixup" in n:
+        return "bwd_seg_fixup"
     if "k_segsum" in n:
         return "segsum_src_bwd" if "<true>" in n else "segsum_dst_fwd"
     table = {"k_edge_init_seg": "edge_init_seg_fwd", "k_edge_init": "edge_init_fwd",
