@@ -263,6 +263,8 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.bslab_elems = bslab;
   W.slab = b.take(4 * std::max<size_t>(slab, 1));
   W.bslab = b.take(4 * std::max<size_t>(bslab, 1));
+  W.slab_b = b.take(4 * std::max<size_t>(slab, 1));  // alternating with slab (gnn_bwd.hip)
+  W.bslab_b = b.take(4 * std::max<size_t>(bslab, 1));
   slab = bslab = 0;
   if (d.F > 0) {
     fit(tn_plan(d.H, d.F, (int)d.N), d.H, d.F);

@@ -33,6 +33,15 @@
 
 #include "epilogues.hpp"
 #include "gemm.hpp"
+#include "reduce.hpp"
+
+// experiment switches (A/B only; 0 = the shipped form)
+#ifndef CGR_EXP_PRIO
+#define CGR_EXP_PRIO 0
+#endif
+#ifndef CGR_EXP_RF2
+#define CGR_EXP_RF2 0
+#endif
 
 namespace cgr {
 
@@ -213,6 +222,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + B3_BK - 1) / B3_BK;
   const int sw = fg ^ lds_swz(fr);  // lds_swz(16 j + fr) == lds_swz(fr)
+  const bool upper = w >= WAVES / 2;  // the second SIMD partner of each wave pair
+  (void)upper;
 
   // ---- A: RF row fragments per lane, two float4 fetches per fragment per k step ----
   typename AL::Row arow[RF];
@@ -372,6 +383,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     __syncthreads();
   };
 
+#if CGR_EXP_PRIO
+  if (upper) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half wins VALU arbitration
+#endif
   {  // prologue: buffers 0, 1 <- B(0), B(1); afr0 <- A(0); raw set 0 <- A(1), B(2)
     ARaw a0, xa0, xa1;
     BRaw b0, b1, xb0, xb1;
@@ -397,6 +411,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     }
   }
 
+#if CGR_EXP_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   // ---- epilogue (the stage buffers are dead after the last barrier) ----
   constexpr int C4 = BN / 4;
   constexpr int EIT = (BM * C4 + NT - 1) / NT;
@@ -521,6 +538,12 @@ inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int
   // finite in-bounds data, multiplied by the image's zero rows)
   auto go = [&](auto NFc) -> hipError_t {
     constexpr int NF = decltype(NFc)::value;
+#if CGR_EXP_RF2
+    // 128-row tiles as 4 waves x 2 row fragments (one wave per SIMD, B fragments read once per
+    // two row fragments)
+    if (K % 4 == 0 && w8)
+      return launch_b3nt_t<4, 2, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
+#endif
     if (K % 4 == 0)
       return w8 ? launch_b3nt_t<8, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st)
                 : launch_b3nt_t<4, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
@@ -709,16 +732,24 @@ struct B3TniShape {
   static constexpr size_t LDS_BYTES = (size_t)2 * SU4 * 16;
 };
 
+// prev (slab == null: none): the previous weight gradient's split-K slabs, reduced by this
+// launch's threads before their own work (the launch-boundary reduce: no reduce launch, and the
+// slab read overlaps other workgroups' main loops; prev's slabs are not this launch's)
 template <int TNN, int TNK, class BL>
 __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
     B3EImg ai, BL bl, float* __restrict__ slab, float* __restrict__ bslab, int Nout, int Kout,
-    int R, int rows_per_split, int tiles_k, int want_bias) {
+    int R, int rows_per_split, int tiles_k, int want_bias, RedJob prev) {
   typedef B3TnSrc<BL> TB;
   using S = B3TniShape<TNN, TNK>;
   constexpr int CW = S::CW, RN = S::RN, RX = S::RX, NA = S::NA, BC = S::BC, SU4 = S::SU4;
   constexpr int JB = S::JB;
   extern __shared__ b3_u4 b3_lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  if (prev.slab) {
+    const int64_t tot = reduce_items(prev);
+    for (int64_t f = (int64_t)blockIdx.x * S::NT + tid; f < tot; f += (int64_t)gridDim.x * S::NT)
+      reduce_slab_item(prev, f);
+  }
   const int lin = xcd_remap(blockIdx.x, gridDim.x);
   const int split = lin / tiles_k, tkk = lin - split * tiles_k;
   const int k0 = tkk * TNK * 16;
@@ -726,6 +757,10 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
   const int e_end = min(R, e_begin + rows_per_split);
   const int nt = e_end > e_begin ? (e_end - e_begin + 31) / 32 : 0;
 
+  // staging waves win the SIMD's issue arbitration against the compute wave they share it with
+  // (static priority, no per-step flips: cdna_hip_programming.md T5; step A/B +0.5 %,
+  // profiles/r03_fold_ab_cfg2.txt)
+  if (w >= CW) __builtin_amdgcn_s_setprio(1);
   if (w >= CW) {
     // ================= staging waves: B of step t + 1 into LDS buffer (t + 1) & 1 =============
     // job (4-column group cg, 4-row group hc): rows 4 hc .. 4 hc + 3 of a step, half of the
@@ -968,14 +1003,15 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
 template <int TNN, int TNK, class BL>
 inline hipError_t launch_b3tni_t(const B3EImg& ai, const BL& bl, const B3TnPlan& p, float* slab,
                                  float* bslab, int Nout, int Kout, int R, bool want_bias,
-                                 hipStream_t st) {
+                                 hipStream_t st, const RedJob& prev) {
   using S = B3TniShape<TNN, TNK>;
   auto kern = gemm_b3tni_kernel<TNN, TNK, BL>;
   static LdsLimit lim;
   const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), 160 * 1024);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(p.tiles_k * p.splits), dim3(S::NT), S::LDS_BYTES, st, ai, bl,
-                     slab, bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0);
+                     slab, bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0,
+                     prev);
   return hipGetLastError();
 }
 
@@ -990,27 +1026,27 @@ inline bool b3tni_ok(const BL& bl, int Nout, int R) {
 template <class BL>
 inline hipError_t launch_b3tni(const B3EImg& ai, const BL& bl, const B3TnPlan& p, float* slab,
                                float* bslab, int Nout, int Kout, int R, bool want_bias,
-                               hipStream_t st) {
+                               hipStream_t st, const RedJob& prev = RedJob{}) {
   constexpr int TNK = 5;
   if (!b3tni_ok(bl, Nout, R) || p.rows_per_split % 32) return hipErrorInvalidValue;
   if (p.tiles_k != (Kout + 16 * b3tn_tnk(Nout) - 1) / (16 * b3tn_tnk(Nout)))
     return hipErrorInvalidValue;  // a plan from b3tn_plan
   switch (p.tnn) {
-    case 25: return launch_b3tni_t<25, TNK>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
-    case 32: return launch_b3tni_t<32, 4>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st);
+    case 25: return launch_b3tni_t<25, TNK>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st, prev);
+    case 32: return launch_b3tni_t<32, 4>(ai, bl, p, slab, bslab, Nout, Kout, R, want_bias, st, prev);
     default: break;
   }
   // other widths: the smallest instantiated fragment count that covers Nout (extra fragments
   // read the image's zero columns and are not stored)
   const int t = p.tnn;
   B3TnPlan q = p;
-  if (t <= 2) { q.tnn = 2; return launch_b3tni_t<2, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
-  if (t <= 4) { q.tnn = 4; return launch_b3tni_t<4, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
-  if (t <= 8) { q.tnn = 8; return launch_b3tni_t<8, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
-  if (t <= 16) { q.tnn = 16; return launch_b3tni_t<16, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
-  if (t <= 25) { q.tnn = 25; return launch_b3tni_t<25, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st); }
+  if (t <= 2) { q.tnn = 2; return launch_b3tni_t<2, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st, prev); }
+  if (t <= 4) { q.tnn = 4; return launch_b3tni_t<4, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st, prev); }
+  if (t <= 8) { q.tnn = 8; return launch_b3tni_t<8, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st, prev); }
+  if (t <= 16) { q.tnn = 16; return launch_b3tni_t<16, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st, prev); }
+  if (t <= 25) { q.tnn = 25; return launch_b3tni_t<25, TNK>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st, prev); }
   q.tnn = 32;
-  return launch_b3tni_t<32, 4>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st);
+  return launch_b3tni_t<32, 4>(ai, bl, q, slab, bslab, Nout, Kout, R, want_bias, st, prev);
 }
 
 }  // namespace cgr

@@ -61,28 +61,46 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
 
 // split-bf16 TN with the n-side operand A [R, Nout] as an e-image (gemm_b3.hpp): A is split
 // once by b3_eimage into `img`, then every k-tile of the GEMM reads it pre-split
+// prev: a previous weight gradient's slab reduction folded into this launch (gemm_b3.hpp)
 template <class BL>
 static hipError_t b3tni_run(const char* name, const void* img, const BL& bl, int Nout, int Kout,
                             int R, float* slab, float* bslab, bool want_bias, TnPlan* plan,
-                            hipStream_t st, int target = kB3TnTarget) {
+                            hipStream_t st, int target = kB3TnTarget,
+                            const RedJob& prev = RedJob{}) {
   const B3TnPlan q = b3tn_plan(Nout, Kout, R, target);
   *plan = TnPlan{1, q.tiles_k, q.splits, q.rows_per_split};
   ProfScope _p(name, st);
   return launch_b3tni(B3EImg{static_cast<const b3_u4*>(img), b3_eimg_cols(Nout)}, bl, q, slab,
-                      bslab, Nout, Kout, R, want_bias, st);
+                      bslab, Nout, Kout, R, want_bias, st, prev);
 }
 
 template <class BL>
 static hipError_t b3tni_gemm(const char* name, const float* A, int64_t lda, void* img,
                              const BL& bl, int Nout, int Kout, int R, float* slab, float* bslab,
                              bool want_bias, TnPlan* plan, hipStream_t st,
-                             int target = kB3TnTarget) {
+                             int target = kB3TnTarget, const RedJob& prev = RedJob{}) {
   {
     ProfScope _p("eimage", st);
     const hipError_t e = b3_eimage(A, lda, R, Nout, static_cast<b3_u4*>(img), st);
     if (e != hipSuccess) return e;
   }
-  return b3tni_run(name, img, bl, Nout, Kout, R, slab, bslab, want_bias, plan, st, target);
+  return b3tni_run(name, img, bl, Nout, Kout, R, slab, bslab, want_bias, plan, st, target, prev);
+}
+
+// a split-K reduction waiting for its launch: folded into the next side-stream split-bf16 TN
+// (the launch-boundary reduce), or launched on its own (flush) before anything that would
+// overwrite its slabs; its gradient bucket's event is recorded once it has run
+struct PendingReduce {
+  RedJob job{};  // job.slab == nullptr: none
+  int bucket = -1;
+};
+static RedJob make_red_job(const TnPlan& p, const float* slab, const float* bslab, int Nout,
+                           int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
+                           int gap_at = 0, int gap_len = 0) {
+  RedJobs js{};
+  add_reduce_job(js, slab, bslab, p.splits, Nout, Kout, dst, ld_dst, col_off, bias_dst, gap_at,
+                 gap_len);
+  return js.n ? js.j[0] : RedJob{};
 }
 
 static hipError_t tn_reduce(const TnPlan& p, const float* slab, const float* bslab, int Nout,
@@ -107,8 +125,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
   float* ds = reinterpret_cast<float*>(ws + WL.ds);
   float* Gs = reinterpret_cast<float*>(ws + WL.Gs);
-  float* slab = reinterpret_cast<float*>(ws + WL.slab);
-  float* bslab = reinterpret_cast<float*>(ws + WL.bslab);
+  // side-stream slab buffers, alternating: a TN writes one while the previous weight gradient's
+  // slabs in the other are reduced in its prologue
+  float* slabs[2] = {reinterpret_cast<float*>(ws + WL.slab),
+                     reinterpret_cast<float*>(ws + WL.slab_b)};
+  float* bslabs[2] = {reinterpret_cast<float*>(ws + WL.bslab),
+                      reinterpret_cast<float*>(ws + WL.bslab_b)};
+  int sb = 0;  // buffer of the next side-stream TN
   float* slab2 = reinterpret_cast<float*>(ws + WL.slab2);
   float* bslab2 = reinterpret_cast<float*>(ws + WL.bslab2);
   float* dsig_part = reinterpret_cast<float*>(ws + WL.dsig_part);
@@ -134,6 +157,46 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
   hipStream_t side = (prof_enabled() || single_stream()) ? st : ss->side;
 
+  PendingReduce pend;
+  auto retire = [&]() -> int {  // pend has run (folded into a TN, or launched)
+    if (pend.job.slab && bucket_events && pend.bucket >= 0)
+      HIP_RET(hipEventRecord(bucket_events[pend.bucket], side));
+    pend = PendingReduce{};
+    return 0;
+  };
+  // launch pend on its own (with `extra`, a job that runs in the same launch, if any)
+  auto flush = [&](const RedJob* extra = nullptr) -> int {
+    RedJobs js{};
+    if (pend.job.slab) js.j[js.n++] = pend.job;
+    if (extra && extra->slab) js.j[js.n++] = *extra;
+    if (js.n == 0) return 0;
+    for (int i = 0; i < js.n; ++i) js.total += js.j[i].nblk;
+    {
+      ProfScope _p("splitk_reduce", side);
+      HIP_RET(reduce_slabs_batched(js, kReduceMaxBlocks, side));
+    }
+    return retire();
+  };
+  // the side TN writing slabs[sb] took pend's job as its prologue; its own becomes pending
+  auto fold = [&](const RedJob& mine, int bucket) -> int {
+    const int rc = retire();
+    if (rc) return rc;
+    pend.job = mine;
+    pend.bucket = bucket;
+    sb ^= 1;
+    return 0;
+  };
+  // a TN that cannot fold (fp32 families, the edge-feature TN): pend and its own reduction in one
+  // launch after it
+  auto unfolded = [&](const RedJob& mine, int bucket) -> int {
+    const int rc = flush(&mine);
+    if (rc) return rc;
+    if (bucket_events && bucket >= 0) HIP_RET(hipEventRecord(bucket_events[bucket], side));
+    sb ^= 1;
+    return 0;
+  };
+
+
   // readout (the head's dwf / dbf sums run on the side stream below)
   {
     ProfScope _p("readout_act_bwd", st);
@@ -150,46 +213,63 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
                        grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], side));
     }
     TnPlan p;
+    float* sl = slabs[sb];
+    float* bsl = bslabs[sb];
+    float* gW = grads[CGR_PARAM_E2N_W(D)];
+    float* gb = grads[CGR_PARAM_E2N_B(D)];
+    // bucket 0 (edge_to_node, ffn): complete once this reduction has run
     if (fv.xp) {  // [xp | s] with x padded to Fp: the pad columns are skipped by the reduce
       const int Fp = d.Fp;
       LdPlain<4> al{dzn, Hp};
       LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
+      const RedJob mine = make_red_job(TnPlan{}, sl, bsl, H, Fp + H, gW, F + H, 0, gb, F, Fp - F);
       if (b3tni_ok(bl, H, N) && ((uintptr_t)fv.xp & 15) == 0) {
-        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl, H, Fp + H, N, slab,
-                           bslab, true, &p, side, kB3TnReadoutTarget));
-      } else if (tnr_x_ok(H, Fp + H, Fp, fv.xp)) {
-        HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
-                                TnrConcat{fv.xp, Fp, fv.a[D], Hp, Fp}, H, Fp + H, N, slab, bslab,
-                                true, &p, side, kTnrReadoutTarget)));
+        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl, H, Fp + H, N, sl, bsl,
+                           true, &p, side, kB3TnReadoutTarget, pend.job));
+        RedJob j = mine;
+        j.splits = p.splits;
+        if (const int rc = fold(j, 0)) return rc;
       } else {
-        HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, slab, bslab, true, &p,
-                        side));
+        if (tnr_x_ok(H, Fp + H, Fp, fv.xp)) {
+          HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
+                                  TnrConcat{fv.xp, Fp, fv.a[D], Hp, Fp}, H, Fp + H, N, sl, bsl,
+                                  true, &p, side, kTnrReadoutTarget)));
+        } else {
+          HIP_RET(tn_gemm("gemm_tn_wgrad_readout", al, bl, H, Fp + H, N, sl, bsl, true, &p,
+                          side));
+        }
+        RedJob j = mine;
+        j.splits = p.splits;
+        if (const int rc = unfolded(j, 0)) return rc;
       }
-      HIP_RET(tn_reduce(p, slab, bslab, H, Fp + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
-                        grads[CGR_PARAM_E2N_B(D)], side, F, Fp - F));
     } else {
       const LdConcat<4> bl4{b->x, F, fv.a[D], Hp, F};
+      const RedJob mine = make_red_job(TnPlan{}, sl, bsl, H, F + H, gW, F + H, 0, gb);
       if (F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 && b3tni_ok(bl4, H, N)) {
-        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl4, H, F + H, N, slab,
-                           bslab, true, &p, side, kB3TnReadoutTarget));
-      } else if (F % 4 == 0 && tnr_x_ok(H, F + H, F, b->x)) {
-        HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
-                                TnrConcat{b->x, F, fv.a[D], Hp, F}, H, F + H, N, slab, bslab,
-                                true, &p, side, kTnrReadoutTarget)));
+        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl4, H, F + H, N, sl, bsl,
+                           true, &p, side, kB3TnReadoutTarget, pend.job));
+        RedJob j = mine;
+        j.splits = p.splits;
+        if (const int rc = fold(j, 0)) return rc;
       } else {
-        hipError_t e = with_vec(vec_for(b->x, F, F), [&](auto VX) {
-          LdPlain<4> al{dzn, Hp};
-          LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
-          return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, slab, bslab, true, &p,
-                         side);
-        });
-        HIP_RET(e);
+        if (F % 4 == 0 && tnr_x_ok(H, F + H, F, b->x)) {
+          HIP_RET((tnr_gemm<5, 4>("gemm_tn_wgrad_readout", TnrRows{dzn, Hp},
+                                  TnrConcat{b->x, F, fv.a[D], Hp, F}, H, F + H, N, sl, bsl, true,
+                                  &p, side, kTnrReadoutTarget)));
+        } else {
+          hipError_t e = with_vec(vec_for(b->x, F, F), [&](auto VX) {
+            LdPlain<4> al{dzn, Hp};
+            LdConcat<decltype(VX)::value> bl{b->x, F, fv.a[D], Hp, F};
+            return tn_gemm("gemm_tn_wgrad_readout", al, bl, H, F + H, N, sl, bsl, true, &p,
+                           side);
+          });
+          HIP_RET(e);
+        }
+        RedJob j = mine;
+        j.splits = p.splits;
+        if (const int rc = unfolded(j, 0)) return rc;
       }
-      HIP_RET(tn_reduce(p, slab, bslab, H, F + H, grads[CGR_PARAM_E2N_W(D)], F + H, 0,
-                        grads[CGR_PARAM_E2N_B(D)], side));
     }
-    // bucket 0 (edge_to_node, ffn): both written on the side stream above
-    if (bucket_events) HIP_RET(hipEventRecord(bucket_events[0], side));
   }
   // main: ds = dzn W_n[:, F:]
   {
@@ -279,28 +359,36 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
                             E, H, H, st));
     }
     if (fork_ev) HIP_RET(hipStreamWaitEvent(side, fork_ev, 0));
-    {  // side: dW_l = dpre^T m_l, db_l = colsum(dpre)
+    {  // side: dW_l = dpre^T m_l, db_l = colsum(dpre); the previous weight gradient's slabs are
+       // reduced in the TN's prologue, this one's by the next TN (bucket D - l complete then)
       LdPlain<4> al{dp, Hp};
       LdGatherDiff<false> bl{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp};
       TnPlan p;
+      float* sl = slabs[sb];
+      float* bsl = bslabs[sb];
+      RedJob mine = make_red_job(TnPlan{}, sl, bsl, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
+                                 grads[CGR_PARAM_CONV_B(l)]);
       const int tf = tnr_layer_frags(H);
       if (b3tni_ok(bl, H, E)) {
-        HIP_RET(b3tni_gemm("gemm_tn_wgrad_layer", dp, Hp, img_side, bl, H, H, E, slab, bslab,
-                           true, &p, side));
-      } else if (tf == 5) {
-        HIP_RET((tnr_gemm<5, 5>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},
-                                TnrDiff{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp}, H, H, E, slab,
-                                bslab, true, &p, side)));
-      } else if (tf == 4) {
-        HIP_RET((tnr_gemm<4, 4>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},
-                                TnrDiff{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp}, H, H, E, slab,
-                                bslab, true, &p, side)));
+        HIP_RET(b3tni_gemm("gemm_tn_wgrad_layer", dp, Hp, img_side, bl, H, H, E, sl, bsl, true,
+                           &p, side, kB3TnTarget, pend.job));
+        mine.splits = p.splits;
+        if (const int rc = fold(mine, D - l)) return rc;
       } else {
-        HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, slab, bslab, true, &p, side));
+        if (tf == 5) {
+          HIP_RET((tnr_gemm<5, 5>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},
+                                  TnrDiff{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp}, H, H, E, sl,
+                                  bsl, true, &p, side)));
+        } else if (tf == 4) {
+          HIP_RET((tnr_gemm<4, 4>("gemm_tn_wgrad_layer", TnrRows{dp, Hp},
+                                  TnrDiff{fv.a[l], fv.h[l], iv.src_s, iv.rev_s, Hp}, H, H, E, sl,
+                                  bsl, true, &p, side)));
+        } else {
+          HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, sl, bsl, true, &p, side));
+        }
+        mine.splits = p.splits;
+        if (const int rc = unfolded(mine, D - l)) return rc;
       }
-      HIP_RET(tn_reduce(p, slab, bslab, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
-                        grads[CGR_PARAM_CONV_B(l)], side));
-      if (bucket_events) HIP_RET(hipEventRecord(bucket_events[D - l], side));
     }
     // main: the rows of tile-crossing dst segments (paired edges) or every row (unpaired)
     ProfScope _p("bwd_seg_fixup", st);
@@ -320,11 +408,15 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dpre0, Hp};
       LdPlain<4> bl{fv.e_s, d.Fep};
       TnPlan p;
-      HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, slab, bslab, true, &p, side,
+      float* sl = slabs[sb];
+      float* bsl = bslabs[sb];
+      HIP_RET(tn_gemm("gemm_tn_wgrad_edge", al, bl, H, Fe, E, sl, bsl, true, &p, side,
                       kEdgeTnTargetWorkgroups));
-      HIP_RET(tn_reduce(p, slab, bslab, H, Fe, gW0, F + Fe, F, gb0, side));
+      // with the last layer's pending reduction, in one launch (bucket D + 1 is recorded at the
+      // join below)
+      return unfolded(make_red_job(p, sl, bsl, H, Fe, gW0, F + Fe, F, gb0), -1);
     }
-    return 0;
+    return flush();
   };
   if (!tail_ev) {
     const int rc = edge_tn();
@@ -381,6 +473,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     ProfScope _p("skip_grad_reduce", st);
     HIP_RET(reduce_partials(dsig_part, nb, sj, st));
   }
+  if (const int rc = flush()) return rc;  // (nothing left unless an edge TN was not run)
   // join: every gradient is complete when the main stream reaches here
   HIP_RET(depend(ss, side, st));
   if (bucket_events) HIP_RET(hipEventRecord(bucket_events[D + 1], st));

@@ -111,6 +111,7 @@ struct WorkspaceLayout {
   size_t bytes;
   size_t dpre, dm, dh0, dzn, ds, Gs, slab, bslab, slab2, bslab2, dsig_part, slab_elems,
       bslab_elems;
+  size_t slab_b, bslab_b;  // the side stream's second slab pair (reductions folded into TNs)
   // split-bf16 e-images (gemm_b3.hpp B3EImg) of the weight gradients' shared operand: dpre_l and
   // dzn on the side stream (one at a time), Gs on the caller's stream
   size_t img_side, img_main;

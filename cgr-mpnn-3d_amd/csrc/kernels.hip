@@ -6,6 +6,7 @@
 #include "common.hpp"
 #include "kernels.hpp"
 #include "bwd_rows.hpp"
+#include "reduce.hpp"
 
 namespace cgr {
 
@@ -641,7 +642,6 @@ hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStr
 // ~40k outputs still give >1000 workgroups.  The bias slabs [splits][Nout] ride along as extra
 // float4-less columns in the last workgroups.
 constexpr int kRedCols = 32, kRedGroups = 8;
-constexpr int kReduceMaxBlocks = 256;  // grouped form grid (A/B: beats 64 and unbounded 4096 by 4-8 %)
 
 // one logical block of one reduction job
 __device__ __forceinline__ void reduce_slab_block(const RedJob& J, int blk, float4 (*part)[kRedCols],
@@ -748,53 +748,9 @@ hipError_t reduce_slabs_batched(const RedJobs& jobs, int max_blocks, hipStream_t
   return hipGetLastError();
 }
 
-// One thread per float4 output (and per bias element): it issues the loads of all splits before
-// summing them in split order (no LDS, no barrier; a workgroup-group form above re-synchronises
-// per logical block and was latency-bound at ~1 TB/s).  Deterministic: fixed order p = 0..S-1.
+// One thread per float4 output (and per bias element): reduce_slab_item (reduce.hpp)
 __global__ __launch_bounds__(256) void k_reduce_slabs_flat(RedJob J) {
-  const int ldk = (J.Kout + 3) & ~3;
-  const int c4n = ldk >> 2;
-  const int64_t nf = (int64_t)J.Nout * c4n;
-  const int64_t f = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (f < nf) {
-    const float4* s4 = reinterpret_cast<const float4*>(J.slab) + f;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    int p = 0;
-    for (; p + 8 <= J.splits; p += 8) {
-      float4 v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] = s4[(int64_t)(p + q) * nf];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        s.x += v[q].x;
-        s.y += v[q].y;
-        s.z += v[q].z;
-        s.w += v[q].w;
-      }
-    }
-    for (; p < J.splits; ++p) {
-      const float4 v = s4[(int64_t)p * nf];
-      s.x += v.x;
-      s.y += v.y;
-      s.z += v.z;
-      s.w += v.w;
-    }
-    const int64_t n = f / c4n;
-    const int k = (int)(f - n * c4n) * 4;
-    float* o = J.dst + n * J.ld_dst + J.col_off;
-    const float tv[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int kk = k + q;
-      if (kk >= J.Kout || (kk >= J.gap_at && kk < J.gap_at + J.gap_len)) continue;
-      o[kk >= J.gap_at + J.gap_len ? kk - J.gap_len : kk] = tv[q];
-    }
-  } else if (J.bias_dst && f - nf < J.Nout) {
-    const int n = (int)(f - nf);
-    float s = 0.f;
-    for (int p = 0; p < J.splits; ++p) s += J.bslab[(int64_t)p * J.Nout + n];
-    J.bias_dst[n] = s;
-  }
+  reduce_slab_item(J, (int64_t)blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // flat form (one thread per output, every split in flight) for short split counts: the grouped

@@ -124,6 +124,8 @@ struct RedJobs {
 bool add_reduce_job(RedJobs& jobs, const float* slab, const float* bslab, int splits, int Nout,
                     int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                     int gap_at = 0, int gap_len = 0);
+// grouped form grid (A/B: beats 64 and unbounded 4096 by 4-8 %)
+constexpr int kReduceMaxBlocks = 256;
 hipError_t reduce_slabs_batched(const RedJobs& jobs, int max_blocks, hipStream_t st);
 // flat: one thread per output with every split's load in flight (the critical-path tail) instead
 // of the bounded-grid grouped form that shares the GPU with the other stream
