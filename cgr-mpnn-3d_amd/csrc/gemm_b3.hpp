@@ -35,14 +35,6 @@
 #include "gemm.hpp"
 #include "reduce.hpp"
 
-// experiment switches (A/B only; 0 = the shipped form)
-#ifndef CGR_EXP_PRIO
-#define CGR_EXP_PRIO 0
-#endif
-#ifndef CGR_EXP_RF2
-#define CGR_EXP_RF2 0
-#endif
-
 namespace cgr {
 
 typedef __bf16 b3_bf16x2 __attribute__((ext_vector_type(2)));
@@ -222,8 +214,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + B3_BK - 1) / B3_BK;
   const int sw = fg ^ lds_swz(fr);  // lds_swz(16 j + fr) == lds_swz(fr)
-  const bool upper = w >= WAVES / 2;  // the second SIMD partner of each wave pair
-  (void)upper;
 
   // ---- A: RF row fragments per lane, two float4 fetches per fragment per k step ----
   typename AL::Row arow[RF];
@@ -383,9 +373,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     __syncthreads();
   };
 
-#if CGR_EXP_PRIO
-  if (upper) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half wins VALU arbitration
-#endif
   {  // prologue: buffers 0, 1 <- B(0), B(1); afr0 <- A(0); raw set 0 <- A(1), B(2)
     ARaw a0, xa0, xa1;
     BRaw b0, b1, xb0, xb1;
@@ -411,9 +398,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     }
   }
 
-#if CGR_EXP_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   // ---- epilogue (the stage buffers are dead after the last barrier) ----
   constexpr int C4 = BN / 4;
   constexpr int EIT = (BM * C4 + NT - 1) / NT;
@@ -538,12 +522,6 @@ inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int
   // finite in-bounds data, multiplied by the image's zero rows)
   auto go = [&](auto NFc) -> hipError_t {
     constexpr int NF = decltype(NFc)::value;
-#if CGR_EXP_RF2
-    // 128-row tiles as 4 waves x 2 row fragments (one wave per SIMD, B fragments read once per
-    // two row fragments)
-    if (K % 4 == 0 && w8)
-      return launch_b3nt_t<4, 2, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
-#endif
     if (K % 4 == 0)
       return w8 ? launch_b3nt_t<8, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st)
                 : launch_b3nt_t<4, 1, NF, true>(al, Bimg, c.nimg, ep, M, N, K, c.tiles, st);
