@@ -216,13 +216,16 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   return f;
 }
 
-// learnable-skip partial sums per layer: the top layer's activation kernel writes one per block;
-// below, the fused layer-backward GEMM one per workgroup and its fixup one per block, the rest 0
+// row tiles x column tiles of the fused layer-backward GEMM (gnn_bwd.hip, ep_bwd.hpp)
+int bwd_seg_tiles(const Dims& d) {
+  return (int)cdiv(d.E, b3nt_rows((int)d.E, d.H)) * b3_cols(d.H).tiles;
+}
+
+// learnable-skip partial sums per layer: the top layer's activation kernel writes one per block,
+// the fused layer-backward GEMM below it two per workgroup (its rows, the crossing segment that
+// starts in its tile: ep_bwd.hpp)
 int bwd_dsig_slots(const Dims& d) {
-  const int rows = b3nt_rows((int)d.E, d.H);
-  const int64_t fused = cdiv(d.E, rows) * b3_cols(d.H).tiles + bwd_seg_fixup_blocks(d.E, d.Hp, rows);
-  const int64_t top = layer_act_bwd_blocks(d.E, d.Hp);
-  return (int)std::max(fused, top);
+  return (int)std::max<int64_t>(2 * (int64_t)bwd_seg_tiles(d), layer_act_bwd_blocks(d.E, d.Hp));
 }
 
 WorkspaceLayout workspace_layout(const Dims& d) {
@@ -274,6 +277,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.slab2 = b.take(4 * std::max<size_t>(slab, 1));
   W.bslab2 = b.take(4 * std::max<size_t>(bslab, 1));
   W.dag = b.take(2 * 4 * N * Hp);  // two, alternating by layer
+  W.cnt = b.take(4 * (N * (size_t)b3_cols(d.H).tiles + 1));
   W.dsig_blocks = bwd_dsig_slots(d);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
   W.bytes = b.off;

@@ -11,11 +11,21 @@
 // summed into da[v] are exactly the output rows of v's dst segment, which is contiguous in the
 // dst-sorted row order.  So the tile sums each dst segment from its accumulators in LDS, turns
 // every row r into dh = da - C[r] in place and applies the activation backward -- da and dm
-// never reach memory.  Segments crossing a tile boundary (at most one at each end) add their
-// partial sums atomically to `dag` (two contributors: order-independent, so deterministic for
-// in-degrees <= rows per tile + 1) and store their raw rows to a.dm; bwd_seg_fixup (kernels.hip)
-// completes those rows after the GEMM.  Unpaired edge lists store every row raw and the fixup does
-// the whole src-CSR form.
+// never reach memory.
+//
+// Segments crossing a row-tile boundary (at most one at each end of a tile) are completed inside
+// the launch by the LAST of their contributing workgroups (cdna_hip_programming.md §6
+// Guideline 16, counter form): each contributor adds its partial sum atomically to `dag` (two
+// contributors: order-independent, so deterministic for in-degrees <= rows per tile + 1) and
+// stores the segment's raw rows write-through (sc1), publishes them (vmcnt drain, barrier: no
+// release fence -- an agent-scope release writes back the XCD's L2, here full of the dpre rows
+// just stored: the fenced form ran each GEMM 15-20 us longer) and draws a ticket from the
+// segment's counter; the workgroup that draws the last ticket reads the partial sums and raw rows
+// with sc1 loads (no acquire) and applies the activation backward to all of the segment's rows,
+// then resets the counter and zeroes the segment's entries of the next layer's `dag` buffer (two
+// buffers alternate by layer).  No workgroup waits for another.  Unpaired edge lists (status bit 2) have no such locality: every
+// workgroup stores its rows raw and the last workgroup of the grid runs the src-CSR form over all
+// nodes (correct, slow: a single workgroup -- the CGR edge order is always paired).
 #pragma once
 
 #include "bwd_rows.hpp"
@@ -23,16 +33,39 @@
 
 namespace cgr {
 
+__device__ __forceinline__ void ep_vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// handed-off words (Guideline 16 R1): agent-scope relaxed atomic stores / loads are the sc1
+// (write-through / L2-bypassing) forms, so the hand-off needs no release or acquire fence
+__device__ __forceinline__ void sc1_store4(float* p, float4 v) {
+  __hip_atomic_store(p, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(p + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float4 sc1_load4(const float* p) {
+  float* q = const_cast<float*>(p);
+  return make_float4(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                     __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                     __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                     __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
 template <bool EDGE_INIT>
 struct EpLayerBwdSeg {
   static constexpr bool kSeg = false;
   static constexpr bool kTile = true;
-  LayerBwdArgs a;     // the layer below (a.dpre written)
-  float* raw;         // [M, Hp] = a.dm: the raw rows of crossing segments, for the fixup
-  const int* dst_s;   // [M] node of each (dst-sorted) row
-  float* dag;         // [nodes, Hp] crossing-segment partial sums of da (zero on entry)
-  const int* status;  // graph prep's status word
-  int M, N;           // rows (edges), columns (hidden)
+  LayerBwdArgs a;      // the layer below (a.dpre written)
+  float* raw;          // [M, Hp]: the raw rows of crossing segments (every row, unpaired)
+  const int* dst_s;    // [M] node of each (dst-sorted) row
+  const int* dst_ptr;  // [nodes + 1] dst CSR of the sorted rows
+  const int* src_list;  // unpaired form: src CSR (src_ptr) of the sorted rows
+  const int* src_ptr;
+  float* dag;          // [nodes, Hp] crossing-segment partial sums of da (zero on entry)
+  float* dag_next;     // the next layer's (or null): completed segments' entries zeroed
+  int* cnt;            // [nodes * tiles_n + 1] tickets (zero on entry, left zero)
+  const int* status;   // graph prep's status word
+  int M, N, nodes, tiles_n;
 
   struct Ctx {};
   __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
@@ -46,14 +79,15 @@ struct EpLayerBwdSeg {
 
   // C: the tile's accumulators [BM][LDC] in LDS (column j of the tile = output column n0 + j);
   // sd[q]: dst of rows m0 - 1 + q (q < BM + 2; distinct negative sentinels outside [0, M)),
-  // followed by 16 floats of scratch;
-  // pv: pre4 of the items (r, c4) = (q / C4, q % C4), q = tid + it * NT
+  // followed by 16 words of scratch; pv: pre4 of the items (r, c4) = (q / C4, q % C4),
+  // q = tid + it * NT; tile_id: this workgroup's tile (tm * tiles_n + tn)
   template <int BM, int BN, int NT, int LDC, int EIT>
   __device__ __forceinline__ void tile(const Pre (&pv)[EIT], float* C, const int* sd, int m0,
                                        int n0, int tile_id, int tid) const {
     constexpr int C4 = BN / 4, NCH = BM / 16;
     const int nrow = min(BM, M - m0);
     const bool paired = (*status & 4) == 0;
+    int* scratch = const_cast<int*>(sd) + BM + 2;  // 16 words
     if (paired) {
       // thread (16-row chunk, float4 column): every segment that STARTS in its chunk (running
       // past the chunk's end as needed) and, for chunk 0, the head segment begun in the
@@ -90,9 +124,9 @@ struct EpLayerBwdSeg {
       }
       __syncthreads();
     }
-    // rows of crossing segments (or every row, unpaired): raw dm[rev(r)] for the fixup; all
-    // others: dh -> the activation backward
-    const int vh = sd[0] == sd[1] ? sd[0] : -3;             // head segment's node, if any
+    // rows of crossing segments (or every row, unpaired): raw dm[rev(r)]; all others: dh -> the
+    // activation backward
+    const int vh = sd[0] == sd[1] ? sd[0] : -3;               // head segment's node, if any
     const int vt = sd[nrow] == sd[nrow + 1] ? sd[nrow] : -3;  // tail segment's node, if any
     const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
     float dsig = 0.f;
@@ -107,24 +141,124 @@ struct EpLayerBwdSeg {
           const int v = sd[r + 1];
           const int64_t i = m0 + r;
           if (!paired || v == vh || v == vt)
-            *reinterpret_cast<float4*>(raw + i * a.Hp + col) = x;
+            sc1_store4(raw + i * a.Hp + col, x);
           else
             bwd_row_apply<EDGE_INIT>(a, i, col, x, key, dsig, pv[it]);
         }
       }
     }
-    if (!EDGE_INIT && a.dsig_part) {  // this workgroup's slot of the learnable-skip partials
-      static_assert(NT / 64 <= 16, "reduction scratch: 16 floats after sd (B3NtShape)");
-      float* red = reinterpret_cast<float*>(const_cast<int*>(sd) + BM + 2);
-      dsig = wave_sum(dsig);
-      if ((tid & 63) == 0) red[tid >> 6] = dsig;
+
+    // ---- hand-off: the last contributor of a crossing segment (or of the grid) completes it ----
+    const int tn = tile_id % tiles_n;
+    float dsig_c[2] = {0.f, 0.f};  // learnable-skip partials of the segments completed here
+    int scratch_f0 = -1, scratch_f1 = -1;
+    if (!paired || vh >= 0 || vt >= 0) {  // uniform over the workgroup
+      ep_vm_drain();  // this wave's partial-sum atomics and raw-row stores
       __syncthreads();
       if (tid == 0) {
+        bool any = false;
+        if (paired) {
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const int v = k == 0 ? vh : (vt != vh ? vt : -3);
+            int done = 0;
+            if (v >= 0) {
+              const int contributors =
+                  (dst_ptr[v + 1] - 1) / BM - dst_ptr[v] / BM + 1;  // row tiles it touches
+              const int t = __hip_atomic_fetch_add(&cnt[(int64_t)v * tiles_n + tn], 1,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              done = t == contributors - 1;
+            }
+            scratch[14 + k] = done ? v : -1;
+            any = any || done;
+          }
+        } else {
+          int* gc = cnt + (int64_t)nodes * tiles_n;
+          const int t = __hip_atomic_fetch_add(gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          any = t == (int)(gridDim.x - 1);
+          scratch[14] = any ? 1 : -1;
+          scratch[15] = -1;
+        }
+        (void)any;
+      }
+      __syncthreads();
+      const int f0 = scratch[14], f1 = scratch[15];
+      scratch_f0 = f0;
+      scratch_f1 = f1;
+      if (paired) {
+        // every row of each completed segment x this tile's columns
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int v = k == 0 ? f0 : f1;
+          if (v < 0) continue;
+          const int ib = dst_ptr[v], ie = dst_ptr[v + 1];
+          const int64_t gv = (int64_t)v * a.Hp;
+          float ds = 0.f;
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the ticket
+          for (int q = tid; q < (ie - ib) * C4; q += NT) {
+            const int i = ib + q / C4, col = n0 + 4 * (q % C4);
+            if (col >= N) continue;
+            const float4 da = sc1_load4(dag + gv + col);
+            const float4 x = sc1_load4(raw + (int64_t)i * a.Hp + col);
+            bwd_row_apply<EDGE_INIT>(a, i, col, f4sub(da, x), key, ds,
+                                     bwd_row_loads<EDGE_INIT>(a, i, col));
+          }
+          dsig_c[k] = ds;
+          if (dag_next)
+            for (int c4 = tid; c4 < C4; c4 += NT)
+              if (n0 + 4 * c4 < N)
+                *reinterpret_cast<float4*>(dag_next + gv + n0 + 4 * c4) = f4zero();
+          if (tid == 0) cnt[(int64_t)v * tiles_n + tn] = 0;
+        }
+      } else if (f0 > 0) {
+        // unpaired: da[v] = sum_{src(e) = v} dm[e] = raw[rev(e)], then every row of v's dst
+        // segment, over all nodes and all columns (this workgroup alone)
+        const int C4all = a.Hp >> 2;
+        for (int64_t q = tid; q < (int64_t)nodes * C4all; q += NT) {
+          const int v = (int)(q / C4all), col = 4 * (int)(q % C4all);
+          float4 da = f4zero();
+          for (int j = src_ptr[v], e = src_ptr[v + 1]; j < e; ++j)
+            da = f4add(da, sc1_load4(raw + (int64_t)a.rev_s[src_list[j]] * a.Hp + col));
+          for (int i = dst_ptr[v], e = dst_ptr[v + 1]; i < e; ++i) {
+            const float4 x = sc1_load4(raw + (int64_t)i * a.Hp + col);
+            bwd_row_apply<EDGE_INIT>(a, i, col, f4sub(da, x), key, dsig,
+                                     bwd_row_loads<EDGE_INIT>(a, i, col));
+          }
+        }
+        if (tid == 0) cnt[(int64_t)nodes * tiles_n] = 0;
+      }
+    }
+
+    // learnable-skip partials, at positions fixed by the data (not by which workgroup finished
+    // last, so their fixed-order sum is deterministic): slot tile_id = this tile's rows; slot
+    // gridDim.x + t = the rows of the crossing segment that STARTS in tile t (written by its
+    // completer; zero when none starts there).  Unpaired: everything is the completer's, in its
+    // own tile slot (all other slots are zero, so the sum is exact whatever the completer).
+    if (!EDGE_INIT && a.dsig_part) {
+      static_assert(NT / 64 <= 8, "reduction scratch: words 0..7 after sd (B3NtShape)");
+      float* red = reinterpret_cast<float*>(scratch);
+      auto block_sum = [&](float x) {
+        x = wave_sum(x);
+        __syncthreads();  // scratch free (flags read, previous sum consumed)
+        if ((tid & 63) == 0) red[tid >> 6] = x;
+        __syncthreads();
         float s = 0.f;
 #pragma unroll
         for (int w = 0; w < NT / 64; ++w) s += red[w];
-        a.dsig_part[tile_id] = s;
-      }
+        return s;
+      };
+      const float st = block_sum(dsig);
+      if (tid == 0) a.dsig_part[tile_id] = st;
+      const int f[2] = {scratch_f0, scratch_f1};
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (paired && f[k] >= 0) {
+          const float sc = block_sum(dsig_c[k]);
+          if (tid == 0)
+            a.dsig_part[gridDim.x + (dst_ptr[f[k]] / BM) * tiles_n + tn] = sc;
+        }
+      const bool starts = paired && vt >= 0 && dst_ptr[vt] >= m0;
+      if (!starts && tid == 0) a.dsig_part[gridDim.x + tile_id] = 0.f;
     }
   }
 };

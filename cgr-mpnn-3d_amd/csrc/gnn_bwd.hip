@@ -12,12 +12,12 @@
 //     dW_l = dpre^T (a_l[src] - h_l[rev])  (message recomputed, never stored) ; db_l = colsum
 //     dm = dpre W_l ; da = segsum_src(dm) ; dh_l = da[dst] - dm[rev] -> the next lower layer's
 //     dpre, all in the dm GEMM's epilogue (EpLayerBwdSeg, ep_bwd.hpp: rows gathered through rev
-//     so each dst segment's rows are the dm rows its node sums; dm and da never stored) plus a
-//     small fixup launch for the segments that cross a row tile (bwd_seg_fixup)
+//     so each dst segment's rows are the dm rows its node sums; dm and da never stored; segments
+//     that cross a row tile completed in the same launch by their last contributor)
 //   dh0 = sum_l s_l dpre_l (every layer's skip term) ; dpre0 = (dh0 + dh_0) * act'(pre0)
 //   dW0[:, F:] = dpre0^T e ; db0 = colsum(dpre0) ; dW0[:, :F] = (segsum_src dpre0)^T x
 //
-// Streams: the critical path is act_bwd -> (dm GEMM + fused epilogue -> fixup) per layer.
+// Streams: the critical path is act_bwd -> the fused dm GEMM per layer.
 // Every weight-gradient TN GEMM (+ its slab reduction) only feeds the gradient outputs, so it runs on the side stream,
 // forked right after its input is produced; every layer's dpre has a buffer of its own (the
 // edge-init backward sums them into dh0), so the main stream waits for the side stream only at
@@ -138,7 +138,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   void* img_side = ws + WL.img_side;
   void* img_main = ws + WL.img_main;
   // partial sums of tile-crossing segments, accumulated by layer l's fused backward GEMM: two
-  // buffers, alternating by layer (each fixup zeroes the next layer's)
+  // buffers, alternating by layer (a segment's completer zeroes its entries of the next one)
   auto dag_of = [&](int l) {
     return reinterpret_cast<float*>(ws + WL.dag) + (l & 1) * (int64_t)d.N * d.Hp;
   };
@@ -282,7 +282,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   const int nb = WL.dsig_blocks;
   // row tile of the fused layer-backward GEMMs: crossing segments accumulate in dag
   const int seg_rows = b3nt_rows(E, H);
-  const int seg_tiles = (int)cdiv(E, seg_rows) * b3_cols(H).tiles;
+  const int seg_cols = b3_cols(H).tiles;
+  const int seg_tiles = bwd_seg_tiles(d);
+  int* cnt = reinterpret_cast<int*>(ws + WL.cnt);
   auto layer_args = [&](int l) {
     uint32_t thresh;
     float scale;
@@ -312,6 +314,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     ProfScope _p("layer_act_bwd", st);
     LayerBwdArgs la = layer_args(D - 1);
     la.dag = dag_of(D - 1);
+    la.cnt = cnt;
+    la.cnt_nodes = N;
+    la.cnt_tiles = seg_cols;
     la.tile_rows = seg_rows;
     HIP_RET(layer_act_bwd(la, nb, st));
   }
@@ -351,11 +356,18 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       const LdGatherRows al{dp, iv.rev_s, Hp};
       const b3_u4* img = static_cast<const b3_u4*>(fv.b3lb[l]);
       float* dg = dag_of(l);
+      float* dgn = l > 0 ? dag_of(l - 1) : nullptr;
       if (l > 0)
-        HIP_RET(launch_b3nt(al, img, EpLayerBwdSeg<false>{lb, dm, iv.dst_s, dg, iv.status, E, H},
+        HIP_RET(launch_b3nt(al, img,
+                            EpLayerBwdSeg<false>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
+                                                 iv.src_ptr, dg, dgn, cnt, iv.status, E, H, N,
+                                                 seg_cols},
                             E, H, H, st));
       else
-        HIP_RET(launch_b3nt(al, img, EpLayerBwdSeg<true>{lb, dm, iv.dst_s, dg, iv.status, E, H},
+        HIP_RET(launch_b3nt(al, img,
+                            EpLayerBwdSeg<true>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
+                                                iv.src_ptr, dg, dgn, cnt, iv.status, E, H, N,
+                                                seg_cols},
                             E, H, H, st));
     }
     if (fork_ev) HIP_RET(hipStreamWaitEvent(side, fork_ev, 0));
@@ -390,11 +402,6 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         if (const int rc = unfolded(mine, D - l)) return rc;
       }
     }
-    // main: the rows of tile-crossing dst segments (paired edges) or every row (unpaired)
-    ProfScope _p("bwd_seg_fixup", st);
-    HIP_RET(bwd_seg_fixup(lb, l == 0, iv.dst_s, iv.dst_ptr, iv.src_list, iv.src_ptr, dag_of(l),
-                          l > 0 ? dag_of(l - 1) : nullptr, iv.status, N, seg_rows, seg_tiles, nb,
-                          st));
   }
   float* gW0 = grads[CGR_PARAM_EDGE_INIT_W];
   float* gb0 = grads[CGR_PARAM_EDGE_INIT_B];
@@ -468,7 +475,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
 
   if (d.learnable_skip) {
     ScalarReduceJobs sj{};
-    for (int l = 0; l < D; ++l) sj.out[l] = grads[CGR_PARAM_SKIP(D, l)];
+    for (int l = 0; l < D; ++l) {
+      sj.out[l] = grads[CGR_PARAM_SKIP(D, l)];
+      // the top layer's activation kernel fills all nb slots, the fused GEMMs two per workgroup
+      sj.count[l] = l == D - 1 ? nb : 2 * seg_tiles;
+    }
     sj.n = D;
     ProfScope _p("skip_grad_reduce", st);
     HIP_RET(reduce_partials(dsig_part, nb, sj, st));

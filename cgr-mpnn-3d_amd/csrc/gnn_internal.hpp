@@ -106,7 +106,7 @@ struct ArenaLayout {
 
 // Backward workspace.  dpre has one buffer per layer (no side->main wait before a buffer is
 // rewritten; the edge-init backward sums dh0 from all of them); dm holds only the rows the fused
-// layer-backward GEMM leaves to its fixup (ep_bwd.hpp).
+// layer-backward GEMM hands to the completer of a tile-crossing segment (ep_bwd.hpp).
 struct WorkspaceLayout {
   size_t bytes;
   size_t dpre, dm, dh0, dzn, ds, Gs, slab, bslab, slab2, bslab2, dsig_part, slab_elems,
@@ -118,9 +118,12 @@ struct WorkspaceLayout {
   // 2 x [N, Hp] partial da sums of the dst segments that cross a row tile of the fused
   // layer-backward GEMM (ep_bwd.hpp), alternating by layer
   size_t dag;
+  // [N * column tiles + 1] ticket counters of those segments (and of the grid, unpaired form)
+  size_t cnt;
   int dsig_blocks;
 };
 int bwd_dsig_slots(const Dims& d);
+int bwd_seg_tiles(const Dims& d);
 
 // Forward variants.  Training (cgr_gnn_forward): every activation the backward reads is saved in
 // the arena and the weight images are packed into it by each call.  Eval (cgr_gnn_predict): no

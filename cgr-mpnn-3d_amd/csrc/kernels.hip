@@ -495,10 +495,14 @@ __global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
     const int64_t nb = cdiv(a.E, a.tile_rows) - 1;  // interior row-tile boundaries
     if (t < nb * C4) {
       const int64_t m = (t / C4 + 1) * a.tile_rows;
-      const int n = 4 * (int)(t % C4);
+      const int c = (int)(t % C4);
       const int v = a.dst_s[m];
-      if (a.dst_s[m - 1] == v) *reinterpret_cast<float4*>(a.dag + (int64_t)v * a.Hp + n) = f4zero();
+      if (a.dst_s[m - 1] == v) {
+        *reinterpret_cast<float4*>(a.dag + (int64_t)v * a.Hp + 4 * c) = f4zero();
+        if (c < a.cnt_tiles) a.cnt[(int64_t)v * a.cnt_tiles + c] = 0;
+      }
     }
+    if (t == 0) a.cnt[a.cnt_nodes * a.cnt_tiles] = 0;  // the grid ticket (unpaired form)
   }
   if (a.dsig_part) block_partial(dsig, a.dsig_part);
 }
@@ -508,93 +512,6 @@ hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st) {
   const int nb = nblocks > need ? nblocks : need;  // extra blocks write zero partials
   if (need <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_layer_bwd, dim3(nb), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
-
-// Completion of the fused layer-backward GEMM (ep_bwd.hpp), grid-stride.  Paired: thread =
-// (interior row-tile boundary m, row slot k < kFixupRows, float4 column); the segment of
-// v = dst(m) crosses the boundary when dst(m - 1) == v and is completed at the first boundary it
-// crosses: da = dag[v] (both partials in), dh = da - dm[rev(i)] for rows i = ib + k, ib + k + 4 ..
-// of the segment (a.dm holds those rows raw); the slot-0 thread zeroes v's entry of the NEXT
-// layer's partial-sum buffer (dag_next: the two alternate, so no thread reads what another
-// zeroes).  Unpaired: thread = (node, float4 column), the src segmented sum da[v] over
-// the raw rows (row r of a.dm is dm[rev(r)], so dm[e] = a.dm[rev(e)]).
-constexpr int kFixupRows = 4;
-template <bool EDGE_INIT>
-__global__ __launch_bounds__(256) void k_bwd_seg_fixup(LayerBwdArgs a, const int* __restrict__ dst_s,
-                                                       const int* __restrict__ dst_ptr,
-                                                       const int* __restrict__ src_list,
-                                                       const int* __restrict__ src_ptr,
-                                                       const float* __restrict__ dag,
-                                                       float* __restrict__ dag_next,
-                                                       const int* __restrict__ status, int64_t N,
-                                                       int tile_rows, int slot0, int nslots) {
-  const int C4 = a.Hp >> 2;
-  const bool paired = (*status & 4) == 0;
-  const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  float dsig = 0.f;
-  auto ld4 = [&](int64_t r, int n) {
-    return *reinterpret_cast<const float4*>(a.dm + r * a.Hp + n);
-  };
-  if (paired) {
-    const int64_t nb = cdiv(a.E, tile_rows) - 1;
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nb * kFixupRows * C4;
-         t += stride) {
-      const int64_t bk = t / C4;
-      const int n = 4 * (int)(t - bk * C4);
-      const int64_t m = (bk / kFixupRows + 1) * tile_rows;
-      const int k = (int)(bk % kFixupRows);
-      const int v = dst_s[m];
-      if (dst_s[m - 1] != v) continue;
-      const int ib = dst_ptr[v], ie = dst_ptr[v + 1];
-      if (ib < m - tile_rows) continue;  // crossed an earlier boundary: completed there
-      const int64_t o = (int64_t)v * a.Hp + n;
-      const float4 da = *reinterpret_cast<const float4*>(dag + o);
-      if (k == 0 && dag_next) *reinterpret_cast<float4*>(dag_next + o) = f4zero();
-      for (int i = ib + k; i < ie; i += kFixupRows)
-        bwd_row_apply<EDGE_INIT>(a, i, n, f4sub(da, ld4(i, n)), key, dsig,
-                                 bwd_row_loads<EDGE_INIT>(a, i, n));
-    }
-  } else {
-    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < N * C4; t += stride) {
-      const int64_t v = t / C4;
-      const int n = 4 * (int)(t - v * C4);
-      float4 da = f4zero();
-      for (int j = src_ptr[v], e = src_ptr[v + 1]; j < e; ++j)
-        da = f4add(da, ld4(a.rev_s[src_list[j]], n));
-      for (int i = dst_ptr[v], e = dst_ptr[v + 1]; i < e; ++i)
-        bwd_row_apply<EDGE_INIT>(a, i, n, f4sub(da, ld4(i, n)), key, dsig,
-                                 bwd_row_loads<EDGE_INIT>(a, i, n));
-    }
-  }
-  if (!EDGE_INIT && a.dsig_part) {
-    block_partial(dsig, a.dsig_part + slot0);
-    for (int64_t s = slot0 + gridDim.x + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-         s < nslots; s += stride)
-      a.dsig_part[s] = 0.f;
-  }
-}
-
-int bwd_seg_fixup_blocks(int64_t E, int Hp, int tile_rows) {
-  const int64_t t = (cdiv(E, tile_rows) - 1) * kFixupRows * (Hp / 4);
-  const int64_t b = cdiv(t, 256);
-  return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
-}
-
-hipError_t bwd_seg_fixup(const LayerBwdArgs& a, bool edge_init, const int* dst_s,
-                         const int* dst_ptr, const int* src_list, const int* src_ptr,
-                         const float* dag, float* dag_next, const int* status, int64_t N,
-                         int tile_rows, int slot0, int nslots, hipStream_t st) {
-  if (N <= 0 || a.E <= 0) return hipSuccess;
-  if (a.Hp % 4 || tile_rows <= 0) return hipErrorInvalidValue;
-  const int nb = bwd_seg_fixup_blocks(a.E, a.Hp, tile_rows);
-  if (edge_init)
-    hipLaunchKernelGGL(k_bwd_seg_fixup<true>, dim3(nb), dim3(256), 0, st, a, dst_s, dst_ptr,
-                       src_list, src_ptr, dag, dag_next, status, N, tile_rows, slot0, nslots);
-  else
-    hipLaunchKernelGGL(k_bwd_seg_fixup<false>, dim3(nb), dim3(256), 0, st, a, dst_s, dst_ptr,
-                       src_list, src_ptr, dag, dag_next, status, N, tile_rows, slot0, nslots);
   return hipGetLastError();
 }
 
@@ -781,7 +698,7 @@ __global__ __launch_bounds__(256) void k_reduce_partials(const float* __restrict
                                                          ScalarReduceJobs jobs) {
   const int j = blockIdx.x;
   float s = 0.f;
-  for (int b = threadIdx.x; b < nb; b += blockDim.x) s += part[(int64_t)j * nb + b];
+  for (int b = threadIdx.x; b < jobs.count[j]; b += blockDim.x) s += part[(int64_t)j * nb + b];
   __shared__ float red[4];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;

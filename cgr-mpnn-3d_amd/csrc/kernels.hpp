@@ -60,7 +60,7 @@ hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_gra
 
 struct LayerBwdArgs {
   // dh_{l+1}: top layer (l == D-1, layer_act_bwd): ds[dst_s[i]]; below (the fused dm GEMM,
-  // ep_bwd.hpp, and its fixup): da[dst(i)] - dm[rev_s[i]], da = segsum_src(dm)
+  // ep_bwd.hpp): da[dst(i)] - dm[rev_s[i]], da = segsum_src(dm)
   const float* ds;
   const float* dm;
   const int* dst_s;
@@ -85,25 +85,17 @@ struct LayerBwdArgs {
   int64_t dpre_stride;
   int nlayers;
   const float* sig[CGR_MAX_DEPTH];
-  // top layer (layer_act_bwd): the entries of dag the fused layer-backward GEMMs accumulate
-  // (nodes whose dst segment crosses a tile_rows row-tile boundary) are zeroed (nullable)
+  // top layer (layer_act_bwd): the entries of dag and of the ticket counters cnt
+  // ([cnt_nodes * cnt_tiles + 1]) the fused layer-backward GEMMs use (nodes whose dst segment
+  // crosses a tile_rows row-tile boundary, ep_bwd.hpp) are zeroed (nullable)
   float* dag;
-  int tile_rows;
+  int* cnt;
+  int64_t cnt_nodes;
+  int tile_rows, cnt_tiles;
 };
 // nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
 hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);
 int layer_act_bwd_blocks(int64_t E, int Hp);
-// Completion of the fused layer-backward GEMM (EpLayerBwdSeg, ep_bwd.hpp; same LayerBwdArgs `a`,
-// a.dm = the raw rows it stored).  Paired edges: the rows of every dst segment that crosses a
-// tile_rows boundary (da = dag[v]; the same entries of dag_next, the buffer the next layer's GEMM
-// accumulates into, are zeroed); unpaired: every node in the src-CSR form.  Learnable-skip
-// partials: one per block at a.dsig_part[slot0 + block], slots up to nslots zero-filled.
-hipError_t bwd_seg_fixup(const LayerBwdArgs& a, bool edge_init, const int* dst_s,
-                         const int* dst_ptr, const int* src_list, const int* src_ptr,
-                         const float* dag, float* dag_next, const int* status, int64_t N,
-                         int tile_rows, int slot0, int nslots, hipStream_t st);
-int bwd_seg_fixup_blocks(int64_t E, int Hp, int tile_rows);
-
 // dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
 // gap_len > 0: slab columns [gap_at, gap_at + gap_len) are padding and skipped; later columns
 // shift down by gap_len in dst (the x | s concat of the readout with x padded to 4 floats)
@@ -136,9 +128,11 @@ hipError_t reduce_slabs(const float* slab, const float* bslab, int splits, int N
 // xp[N, ldp] = x[N, F] with zero padding columns [F, ldp) (16-byte rows for the GEMM loaders)
 hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStream_t st);
 
-// out[j][0] = sum_b part[j * nb + b]   for j < njobs (scalar grads of skip weights)
+// out[j][0] = sum_{b < count[j]} part[j * nb + b]   for j < njobs (scalar grads of skip weights)
+// (the first count[j] of the nb slots of job j)
 struct ScalarReduceJobs {
   float* out[64];
+  int count[64];
   int n;
 };
 hipError_t reduce_partials(const float* part, int nb, const ScalarReduceJobs& jobs,

@@ -7,7 +7,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-ab3}
-MIDS=${MIDS:-seg}
+MIDS=${MIDS-}
 mkdir -p "gpurun_out/$TAG"
 for lib in $([ "${TEST_MIDS:-1}" = 1 ] && for m in $MIDS; do echo build/variants/$m/libcgr_mpnn3d.so; done) ""; do
   if [ -n "$lib" ]; then export CGR_MPNN3D_LIB=$lib; else unset CGR_MPNN3D_LIB; fi
