@@ -685,3 +685,45 @@ def test_backward_refuses_unprepared_arena(cuda_device):
     prepared.backward(dy, params)
     with pytest.raises(RuntimeError, match="CGR_TRAIN_FOR_BACKWARD"):
         bare.backward(dy, params)
+
+
+def _hub_batch(leaves, seed):
+    """Star-shaped reactions: graph g has a hub atom bonded to leaves[g] leaf atoms (bond k =
+    edges 2k, 2k+1, the CGR pair order), so the hub's dst segment has leaves[g] rows: with
+    64- or 128-row tiles it spans two to six row tiles of the fused layer-backward GEMM, whose
+    crossing segments are completed by their last contributing workgroup (ep_bwd.hpp: tickets
+    above two, a middle tile whose head and tail are the same segment, learnable-skip slots of
+    a segment that starts several tiles back)."""
+    from cgr_mpnn_3D._amd.synth import RxnBatch
+
+    rng = np.random.default_rng(seed)
+    xs, eis, eas, bt, ptr = [], [], [], [], [0]
+    for g, k in enumerate(leaves):
+        off = ptr[-1]
+        ei = []
+        for j in range(1, k + 1):
+            ei += [(off + j, off), (off, off + j)]
+        eis.append(np.array(ei, np.int64).T)
+        xs.append(rng.standard_normal((k + 1, 21)).astype(np.float32))
+        eas.append(rng.standard_normal((len(ei), 14)).astype(np.float32))
+        bt.append(np.full(k + 1, g, np.int64))
+        ptr.append(off + k + 1)
+    y = rng.normal(80.0, 20.0, len(leaves)).astype(np.float32)
+    return RxnBatch(x=np.concatenate(xs), edge_index=np.ascontiguousarray(np.concatenate(eis, 1)),
+                    edge_attr=np.concatenate(eas), batch=np.concatenate(bt),
+                    ptr=np.array(ptr, np.int64), y=y)
+
+
+@pytest.mark.parametrize("skip", [True, False])
+def test_hub_segments_spanning_tiles_vs_oracle(skip, cuda_device):
+    # 64-row tiles (few workgroups): hub in-degrees 150 / 70 / 300 span 3-6 tiles
+    b = _hub_batch([150, 3, 70, 300, 5], seed=41)
+    assert _pair_status(b, cuda_device) == 0
+    _oracle_compare(b, 64, 3, "relu", skip, cuda_device)
+
+
+def test_hub_segments_spanning_128_row_tiles_vs_oracle(cuda_device):
+    # >= 96 workgroups: 128-row tiles; in-degrees 130-400 (2-4 tiles per hub segment)
+    b = _hub_batch([130 + (37 * g) % 271 for g in range(48)], seed=42)
+    assert b.edge_index.shape[1] >= 96 * 128
+    _oracle_compare(b, 48, 2, "relu", True, cuda_device)
