@@ -181,7 +181,7 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
 // all those edges (the per-edge kernel reloaded it for every edge: 14 float4 + 14 scalar loads
 // per output float4), and sums its edges' h0 into a_0 in edge order -- the same adds, in the same
 // order, as k_edge_init followed by k_segsum_v4<false>, so h0 / pre0 / a_0 are bitwise unchanged.
-constexpr int kEiNodes = 4;
+constexpr int kEiNodes = 4;  // (2: A/B -0.5 %)
 constexpr int kEiMaxFe = 16;
 
 template <bool REG>
@@ -204,55 +204,78 @@ __global__ __launch_bounds__(128) void k_edge_init_seg(
   }
   const int64_t v0 = (int64_t)blockIdx.x * kEiNodes;
   const int64_t v1 = v0 + kEiNodes < N ? v0 + kEiNodes : N;
-  for (int64_t v = v0; v < v1; ++v) {
-    float4 acc = f4zero();
-    const int ie = dst_ptr[v + 1];
-    for (int i = dst_ptr[v]; i < ie; ++i) {
-      float4 z = *reinterpret_cast<const float4*>(P + (int64_t)src_s[i] * Hp + n);
-      z.x += bias.x;
-      z.y += bias.y;
-      z.z += bias.z;
-      z.w += bias.w;
+  // one edge: P row (gathered) + bias + e W0e^T -> pre0, h0 (loads come from ld())
+  struct EdgeIn {
+    float4 p;
+    float4 e[kEiMaxFe / 4];
+  };
+  auto ld = [&](int i) {
+    EdgeIn x;
+    x.p = *reinterpret_cast<const float4*>(P + (int64_t)src_s[i] * Hp + n);
+    if constexpr (REG) {
       const float* er = e_s + (int64_t)i * Fep;
-      if constexpr (REG) {
 #pragma unroll
-        for (int q4 = 0; q4 < kEiMaxFe / 4; ++q4) {
-          if (4 * q4 >= Fe) break;
-          const float4 ev = *reinterpret_cast<const float4*>(er + 4 * q4);
-          const float e4[4] = {ev.x, ev.y, ev.z, ev.w};
+      for (int q4 = 0; q4 < kEiMaxFe / 4; ++q4)
+        x.e[q4] = 4 * q4 < Fe ? *reinterpret_cast<const float4*>(er + 4 * q4) : f4zero();
+    }
+    return x;
+  };
+  auto edge = [&](int i, const EdgeIn& x) {
+    float4 z = x.p;
+    z.x += bias.x;
+    z.y += bias.y;
+    z.z += bias.z;
+    z.w += bias.w;
+    if constexpr (REG) {
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            if (4 * q4 + k >= Fe) break;
-            const float4 wq = w[4 * q4 + k];
-            z.x += e4[k] * wq.x;
-            z.y += e4[k] * wq.y;
-            z.z += e4[k] * wq.z;
-            z.w += e4[k] * wq.w;
-          }
-        }
-      } else {
-        for (int q = 0; q < Fe; ++q) {
-          const float ev = er[q];
-          const float4 wq = *reinterpret_cast<const float4*>(w0eT + (int64_t)q * Hp + n);
-          z.x += ev * wq.x;
-          z.y += ev * wq.y;
-          z.z += ev * wq.z;
-          z.w += ev * wq.w;
+      for (int q4 = 0; q4 < kEiMaxFe / 4; ++q4) {
+        if (4 * q4 >= Fe) break;
+        const float e4[4] = {x.e[q4].x, x.e[q4].y, x.e[q4].z, x.e[q4].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          if (4 * q4 + k >= Fe) break;
+          const float4 wq = w[4 * q4 + k];
+          z.x += e4[k] * wq.x;
+          z.y += e4[k] * wq.y;
+          z.z += e4[k] * wq.z;
+          z.w += e4[k] * wq.w;
         }
       }
-      const int64_t o = (int64_t)i * Hp + n;
-      if (pre0) *reinterpret_cast<float4*>(pre0 + o) = z;
-      float4 h;
-      h.x = act_fwd(z.x, act);
-      h.y = act_fwd(z.y, act);
-      h.z = act_fwd(z.z, act);
-      h.w = act_fwd(z.w, act);
-      *reinterpret_cast<float4*>(h0 + o) = h;
-      acc = f4add(acc, h);
+    } else {
+      const float* er = e_s + (int64_t)i * Fep;
+      for (int q = 0; q < Fe; ++q) {
+        const float ev = er[q];
+        const float4 wq = *reinterpret_cast<const float4*>(w0eT + (int64_t)q * Hp + n);
+        z.x += ev * wq.x;
+        z.y += ev * wq.y;
+        z.z += ev * wq.z;
+        z.w += ev * wq.w;
+      }
     }
+    const int64_t o = (int64_t)i * Hp + n;
+    if (pre0) *reinterpret_cast<float4*>(pre0 + o) = z;
+    float4 h;
+    h.x = act_fwd(z.x, act);
+    h.y = act_fwd(z.y, act);
+    h.z = act_fwd(z.z, act);
+    h.w = act_fwd(z.w, act);
+    *reinterpret_cast<float4*>(h0 + o) = h;
+    return h;
+  };
+  for (int64_t v = v0; v < v1; ++v) {
+    float4 acc = f4zero();
+    const int ib = dst_ptr[v], ie = dst_ptr[v + 1];
+    // the node's edges two at a time, both edges' loads issued before either is used (a chain
+    // of single edges serialised src index -> P row -> store per edge); summed in edge order
+    int i = ib;
+    for (; i + 2 <= ie; i += 2) {
+      const EdgeIn x0 = ld(i), x1 = ld(i + 1);
+      acc = f4add(acc, edge(i, x0));
+      acc = f4add(acc, edge(i + 1, x1));
+    }
+    if (i < ie) acc = f4add(acc, edge(i, ld(i)));
     *reinterpret_cast<float4*>(a + v * Hp + n) = acc;
     if (zero.n > 0) {
-      const int ib = dst_ptr[v];
       if (ie == ib || ib / zero.tile_rows != (ie - 1) / zero.tile_rows)
         for (int l = 0; l < zero.n; ++l)
           *reinterpret_cast<float4*>(zero.a[l] + v * Hp + n) = f4zero();
