@@ -114,9 +114,6 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     # backward (1: + the D layers' dpre summed into dh0): per launch on average 4 E*H + H*H floats
     add("gemm_nt_layer_bwd_seg", D, 2.0 * E * H * H + E * H,
         f4 * (4 * E * H + H * H) + i4 * (2 * E))
-    # its fixup: the dst segments crossing a 128-row tile (about one per tile, E/N rows each):
-    # the raw rows, their mask and the dpre rows written
-    add("bwd_seg_fixup", D, 0.0, f4 * (E / 128.0) * (E / max(N, 1)) * 3 * H + i4 * 2 * (E / 128.0))
     add("segsum_src_bwd", 1, E * H, seg_dst + i4 * E)  # Gs = segsum_src(dpre0) for dW0[:, :F]
     add("gemm_tn_wgrad_edge", 1, 2.0 * E * H * Fe, f4 * (E * H + E * Fe + H * Fe + H))
     add("gemm_tn_wgrad_node", 1, 2.0 * N * H * F, f4 * (N * H + N * F + H * F))

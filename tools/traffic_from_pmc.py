@@ -65,8 +65,6 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
         if m and m.group(1) != "4":
             return "gemm_tn_wgrad_node"
         return "gemm_tn_wgrad_edge"  # ambiguous only when F % 4 == 0; see note in the output
-    if "k_bwd_seg_fixup" in n:
-        return "bwd_seg_fixup"
     if "k_segsum" in n:
         return "segsum_src_bwd" if "<true>" in n else "segsum_dst_fwd"
     table = {"k_edge_init_seg": "edge_init_seg_fwd", "k_edge_init": "edge_init_fwd",
