@@ -727,3 +727,19 @@ def test_hub_segments_spanning_128_row_tiles_vs_oracle(cuda_device):
     b = _hub_batch([130 + (37 * g) % 271 for g in range(48)], seed=42)
     assert b.edge_index.shape[1] >= 96 * 128
     _oracle_compare(b, 48, 2, "relu", True, cuda_device)
+
+
+def test_unpaired_edge_order_128_row_tiles_vs_oracle(cuda_device):
+    # >= 96 workgroups (128-row tiles): the unpaired form's grid-wide last arriver of the fused
+    # layer backward (ep_bwd.hpp) completes every row while ~100 other workgroups exit
+    from dataclasses import replace
+
+    b = make_batch(220, n_atoms=30, n_bonds=30, n_mace=16, seed=29)
+    per = b.edge_index.shape[1] // b.num_graphs
+    rng = np.random.default_rng(6)
+    order = np.concatenate([g * per + rng.permutation(per) for g in range(b.num_graphs)])
+    u = replace(b, edge_index=np.ascontiguousarray(b.edge_index[:, order]),
+                edge_attr=np.ascontiguousarray(b.edge_attr[order]))
+    assert u.edge_index.shape[1] >= 96 * 128
+    assert _pair_status(u, cuda_device) == 4
+    _oracle_compare(u, 48, 2, "relu", True, cuda_device)
