@@ -29,6 +29,7 @@ __device__ __forceinline__ void b3_pack_job(const B3PackJob& J, int64_t first, i
     for (int j = 0; j < 8; ++j) {
       const int k = ks * B3_BK + b3_kperm(c, j);
       f[j] = (nl < J.N && k < J.K) ? J.src[(int64_t)nl * J.ldn + (int64_t)k * J.ldk] : 0.f;
+      if (J.kscale && k < J.K) f[j] *= J.kscale[k];
     }
     b3_u4 pc[3];
     b3_split8<3>(f, pc);

@@ -56,6 +56,26 @@ struct EpStore {
   }
 };
 
+// C[r, :] = s_r * acc with s_r = dy[node_graph[r]] (readout backward ds = dzn W_n[:, F:], the
+// row factor of dzn; LdActGrad).  Internal [M, ld] buffers, ld % 4 == 0.
+struct EpStoreRowScale {
+  static constexpr bool kSeg = false;
+  float* C;
+  int64_t ld;
+  int M, N;
+  const float* dy;
+  const int* node_graph;
+  struct Ctx {};
+  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  typedef float Pre;
+  __device__ __forceinline__ Pre pre4(int r, int) const { return dy[node_graph[min(r, M - 1)]]; }
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, Pre s, const Ctx&) const {
+    if (r >= M || c >= N) return;
+    *reinterpret_cast<float4*>(C + (int64_t)r * ld + c) =
+        make_float4(s * v.x, s * v.y, s * v.z, s * v.w);
+  }
+};
+
 // D-MPNN layer (GNN.py:91-102):
 //   pre = (m W^T + b) + sigma * h0 ; h = dropout(act(pre))
 struct EpLayer {

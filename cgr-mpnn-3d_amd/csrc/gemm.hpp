@@ -131,6 +131,35 @@ struct LdGatherRows {
   __device__ __forceinline__ float4 combine_nm(const Raw& v) const { return v; }
 };
 
+// the activation-derivative factor of the readout backward's dzn (GNN.py:134-136 reversed):
+// A(v, k) = act'(m[v, k]) with m = hn (ReLU: hn > 0) or zn (internal [M, ld] buffers, ld % 4 == 0).
+// dzn = dy[graph(v)] wf[k] act'(zn[v, k]) factors into this, a per-k scale folded into the weight
+// image (B3PackJob::kscale) and a per-row scale applied by the epilogue (EpStoreRowScale).
+struct LdActGrad {
+  const float* m;
+  int64_t ld;
+  int act;
+  struct Row {
+    const float* p;
+    bool ok;
+  };
+  typedef float4 Raw;
+  __device__ __forceinline__ Row row(int r, int limit) const {
+    const bool ok = r < limit;
+    return Row{m + (int64_t)(ok ? r : 0) * ld, ok};
+  }
+  __device__ __forceinline__ Raw fetch(const Row& rw, int k, int K) const {
+    return *reinterpret_cast<const float4*>(rw.p + (k < K ? k : 0));
+  }
+  __device__ __forceinline__ float4 combine_nm(const Raw& v) const {
+    return make_float4(act_grad(v.x, act), act_grad(v.y, act), act_grad(v.z, act),
+                       act_grad(v.w, act));
+  }
+  __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
+    return mask4(combine_nm(v), rw.ok, k, K);
+  }
+};
+
 // B rows of two stacked weight matrices: rows [0, n0) from base0 (ld0), rows [n0, ...) from base1
 // (ld1).  Used for the merged x-GEMM  x @ [W0[:, :F]; W_n[:, :F]]^T.  VEC divides ld0, ld1, K.
 template <int VEC>

@@ -136,12 +136,13 @@ inline int b3_nk(int K) { return (K + B3_BK - 1) / B3_BK; }
 inline size_t b3_img_u4(int N, int K) { return (size_t)b3_nk(K) * 3 * b3_cols(N).nimg * 4; }
 
 // one pack job: image rows [n_begin, n_begin + rows) from B(n, k) = src[n * ldn + k * ldk]
-// (n < N real rows of this job, zero beyond; k < K real, zero beyond)
+// (n < N real rows of this job, zero beyond; k < K real, zero beyond), times kscale[k] when set
 struct B3PackJob {
   const float* src;
   int64_t ldn, ldk;
   b3_u4* img;
   int n_begin, rows, N, K, nimg, nk;
+  const float* kscale;
 };
 constexpr int kMaxB3PackJobs = 24;  // per launch (kernel-argument size); b3_pack_all splits
 struct B3PackJobs {

@@ -197,20 +197,20 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   };
 
 
-  // readout (the head's dwf / dbf sums run on the side stream below)
-  {
-    ProfScope _p("readout_act_bwd", st);
-    HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
-                            Hp, d.act, dzn, st));
-  }
-  // side: dwf, dbf; dW_n = dzn^T [x | s], db_n (forked before the main stream's readout NT:
-  // deferring it behind a layer, or enqueuing the NT first, A/B -4..-14 %)
+  // side: dwf, dbf; dzn; dW_n = dzn^T [x | s], db_n (forked before the main stream's readout NT:
+  // deferring it behind a layer, or enqueuing the NT first, A/B -4..-14 %).  dzn is materialised
+  // for the weight gradient only: the main stream's NT forms it inside the GEMM (LdActGrad).
   {
     HIP_RET(fork_to(ss, st, side));
     {  // dwf = dy^T g, dbf: off the main chain (step A/B +0.8 %)
       ProfScope _p("head_bwd", side);
       HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
                        grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], side));
+    }
+    {
+      ProfScope _p("readout_act_bwd", side);
+      HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
+                              Hp, d.act, dzn, side));
     }
     TnPlan p;
     float* sl = slabs[sb];
@@ -271,11 +271,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       }
     }
   }
-  // main: ds = dzn W_n[:, F:]
+  // main: ds = dzn W_n[:, F:] = diag(dy[graph]) act'(zn) (diag(wf) W_n[:, F:]) -- the row factor in
+  // the epilogue, the column factor in the weight image (gnn_fwd.hip), act' in the A loader
   {
     ProfScope _p("gemm_nt_readout_bwd", st);
-    HIP_RET(launch_b3nt(LdPlain<4>{dzn, Hp}, static_cast<const b3_u4*>(fv.b3rob),
-                        EpStore{ds, Hp, N, H, nullptr}, N, H, H, st));
+    HIP_RET(launch_b3nt(LdActGrad{d.act == ACT_RELU ? fv.hn : fv.zn, Hp, d.act},
+                        static_cast<const b3_u4*>(fv.b3rob),
+                        EpStoreRowScale{ds, Hp, N, H, dy, iv.node_graph}, N, H, H, st));
   }
 
   // learnable-skip partial-sum slots per layer (bwd_dsig_slots)

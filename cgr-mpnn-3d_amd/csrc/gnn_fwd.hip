@@ -145,7 +145,9 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     for (int l = 0; l < D; ++l)
       HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l]), st));
     if (training & CGR_TRAIN_FOR_BACKWARD) {  // the backward NT GEMMs' W^T images
-      HIP_RET(b3_pack_add(pm, b3_job(Wn + F, 1, F + H, H, H, fv.b3rob), st));
+      B3PackJob rob = b3_job(Wn + F, 1, F + H, H, H, fv.b3rob);  // scaled by wf: LdActGrad
+      rob.kscale = params[CGR_PARAM_FFN_W(D)];
+      HIP_RET(b3_pack_add(pm, rob, st));
       for (int l = 0; l < D; ++l)
         HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l]), st));
     }

@@ -80,7 +80,7 @@ struct FloatView {
   // split-bf16 weight images (gemm_b3.hpp), packed once per step by the forward:
   void* b3x;                      // [W0[:, :F]; W_n[:, :F]]   (x-GEMM)
   void* b3rof;                    // W_n[:, F:]                 (readout forward)
-  void* b3rob;                    // W_n[:, F:]^T               (readout backward)
+  void* b3rob;                    // W_n[:, F:]^T diag(wf)      (readout backward)
   void* b3lf[CGR_MAX_DEPTH];      // W_l                        (layer forward)
   void* b3lb[CGR_MAX_DEPTH];      // W_l^T                      (layer backward)
 };
