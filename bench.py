@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=30)
-    ap.add_argument("--config", default="cfg2", choices=["cfg1", "cfg2", "cfg4", "cfg5"])
+    ap.add_argument("--config", default="cfg2",
+                    choices=["cfg1", "cfg2", "cfg4", "cfg5", "train_default"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a HIP graph (1/0; -1 = auto: on for N = 1)")
     ap.add_argument("--loss", default="fused", choices=["fused", "torch"],
@@ -150,7 +151,7 @@ def roofline_entry(name, work, launches, ms_total, traffic):
       * everything else: algorithmic bytes against HBM.
     Every class also carries `hbm_frac` = algorithmic bytes / time / 8 TB/s beside it."""
     t = ms_total * 1e-3 / launches
-    k = BF16_PRODUCTS.get(name)
+    k = BF16_PRODUCTS.get(name)  # None for the "[f32]" / "[tnr]" fallback families
     hbm = work["bytes"] / t / 1e9
     if k:
         ach, peak, unit, bound = k * work["flops"] / t / 1e12, BF16_MFMA_PEAK_TFLOPS, "TFLOP/s", "mfma"
@@ -448,6 +449,7 @@ def main():
         step()
     torch.cuda.synchronize()
     run = step
+    g = None
     if args.graph and distributed and args.dist_backend != "nccl":
         args.graph = 0  # a gloo collective cannot be recorded into a HIP graph (host copies)
     if args.graph:
@@ -506,13 +508,17 @@ def main():
             except Exception:  # noqa: BLE001
                 traffic = {}
 
+        def base(name):  # "<class>[f32]" / "[tnr]": the fp32 fallback family of a class
+            return name.split("[")[0]
+
         def hbm(name):
-            t = traffic.get(name)
+            t = traffic.get(base(name))
             return None if t is None else t.get("hbm_bytes_per_launch")
 
         for name, (cnt, tot) in rep.items():
             breakdown[name] = {"launches_per_step": cnt / args.profile_steps,
                                "ms_per_step": round(tot / args.profile_steps, 5)}
+        work.update({k: work[base(k)] for k in rep if k not in work and base(k) in work})
         cands = [k for k in rep if k in work]
         if cands:
             dom = max(cands, key=lambda k: rep[k][1])
@@ -595,7 +601,12 @@ def main():
             out["speedup_vs_cpu_baseline"] = round(value / cpu["value"], 2)
         print(json.dumps(out), flush=True)
     if distributed:
-        dist.destroy_process_group()
+        # captured graph (it recorded the per-bucket collectives) first, then the communicator
+        # (ddp.teardown explains the order)
+        from cgr_mpnn_3D._amd.ddp import teardown
+
+        run = g = None  # noqa: F841
+        teardown(model)
 
 
 if __name__ == "__main__":

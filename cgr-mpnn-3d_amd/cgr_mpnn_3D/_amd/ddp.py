@@ -56,6 +56,17 @@ class GradAllReduce:
         else:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
+    def close(self):
+        """Synchronise and drop the communication streams and bucket events (teardown, before
+        ``dist.destroy_process_group``: see ``teardown``)."""
+        for st in self._streams.values():
+            st.synchronize()
+        for evs in self._events.values():
+            for e in evs:
+                e.synchronize()
+        self._streams.clear()
+        self._events.clear()
+
     def __call__(self, flat, buckets, events):
         if events is None or not flat.is_cuda:
             for a, b in buckets:
@@ -80,8 +91,41 @@ def install_grad_allreduce(model, group=None, op=None):
 
 
 def remove_grad_allreduce(model):
+    hook = getattr(model, "_grad_bucket_hook", None)
+    if hook is not None and hasattr(hook, "close"):
+        hook.close()
     model._grad_bucket_hook = None
     return model
+
+
+def teardown(model=None):
+    """End data parallelism in the order the communicator needs, then destroy the process group.
+
+    A collective captured into a HIP graph leaves RCCL state tied to that graph: RCCL attaches a
+    destructor (a graph user object, ``hipGraphRetainUserObject``) that hands the captured
+    collective's launch plan back to its communicator when the graph is destroyed.  Destroying
+    the communicator while such a graph is alive -- what ``bench.py`` did (round 3: the captured
+    step ``g`` was still referenced at ``destroy_process_group``) -- lets that destructor run
+    against a freed communicator later, at interpreter exit: an intermittent abort after all the
+    work had succeeded.  So, in this order: the caller drops every captured graph that recorded a
+    collective (and any bound ``g.replay``) BEFORE calling this; here the device is synchronised,
+    reference cycles are collected (the graph destructors run now, while the communicator lives),
+    the device is synchronised again, the gradient hook's communication streams and events are
+    released, the ranks meet at a barrier and only then is the process group destroyed."""
+    import gc
+
+    if not dist.is_initialized():
+        return
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    gc.collect()
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    if model is not None:
+        remove_grad_allreduce(model)
+    if dist.get_world_size() > 1:
+        dist.barrier()
+    dist.destroy_process_group()
 
 
 def shard_ranges(graph_edges: np.ndarray, world: int) -> list[tuple[int, int]]:

@@ -155,42 +155,17 @@ class GNNFunction(torch.autograd.Function):
         return (None,) * 12 + tuple(grads)
 
 
-class ImageCache:
-    """Split-bf16 forward weight images of one model (cgr_gnn_pack_images), re-packed only when a
-    parameter changed: the key holds every parameter's storage pointer and autograd version
-    counter (bumped by optimizer steps and load_state_dict, which update in place)."""
-
-    def __init__(self):
-        self.key = None
-        self.images = None
-
-    def get(self, cfg, params, dev):
-        key = (str(dev), (cfg.num_node_features, cfg.num_edge_features, cfg.hidden, cfg.depth),
-               tuple((p.data_ptr(), p._version) for p in params))
-        if key != self.key:
-            lib = native.load()
-            n = lib.cgr_gnn_image_bytes(ctypes.byref(cfg))
-            if n < 0:
-                native.check(1)
-            if self.images is None or self.images.numel() < n or self.images.device != dev:
-                self.images = torch.empty(n, dtype=torch.uint8, device=dev)
-            with native.device_guard(dev):
-                native.check(lib.cgr_gnn_pack_images(ctypes.byref(cfg), _param_table(params),
-                                                     native.ptr(self.images),
-                                                     native.stream_ptr(dev)))
-            self.key = key
-        return self.images
-
-
 def gnn_predict(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, dropout_ps,
-                seed, training, params, cache, rng_counter=None):
-    """Forward-only GNN (cgr_gnn_predict): no saved activations, cached weight images.  What
-    GNN.forward runs when no gradient is wanted (test.py:100-113 under torch.no_grad())."""
+                seed, training, params, rng_counter=None):
+    """Forward-only GNN (cgr_gnn_predict): no saved activations.  What GNN.forward runs when no
+    gradient is wanted (test.py:100-113 under torch.no_grad()).  The weight images are packed
+    into the call's own arena by every call: no cache to go stale when an optimizer (FusedAdam,
+    a replayed captured step) updates the parameters through raw pointers, and no buffer shared
+    with a predict still running on another stream."""
     lib = native.load()
     cfg = make_config(*cfg_tuple)
     N, E, B = int(x.shape[0]), int(edge_index.shape[1]), int(num_graphs)
     dev = x.device
-    images = cache.get(cfg, params, dev)
     nbytes = lib.cgr_gnn_predict_arena_bytes(ctypes.byref(cfg), N, E, B)
     if nbytes < 0:
         native.check(1)
@@ -201,7 +176,7 @@ def gnn_predict(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graph
         native.check(lib.cgr_gnn_predict(
             ctypes.byref(cfg), _param_table(params), ctypes.byref(bs),
             _dropout_array(dropout_ps, cfg.depth), ctypes.c_uint64(seed), native.ptr(rng_counter),
-            native.TRAIN_DROPOUT if training else 0, native.ptr(images), native.ptr(arena),
+            native.TRAIN_DROPOUT if training else 0, None, native.ptr(arena),
             native.ptr(y), native.stream_ptr(dev)))
     if _config.strict:
         raise_on_status(arena, cfg, N, E, B, predict=True)

@@ -4,8 +4,7 @@ The reference evaluates one reaction at a time: ``test.py:85-113`` (DataLoader b
 ``cli_tool/activation_energy_predictor.py:71-80`` (per-graph loop, ``batch=None``), both under
 ``torch.no_grad()`` in eval mode.  Both work unchanged on the native module, whose no-grad calls
 take the forward-only path (``cgr_gnn_predict``: no saved activations -- rings of two h and three
-a buffers -- and split-bf16 weight images packed once per parameter version,
-``functional.ImageCache``), but each call is still a ~20-launch forward for ~30 atoms.
+a buffers), but each call is still a ~20-launch forward for ~30 atoms.
 ``predict`` runs that path over large device-collated batches (``GraphStore.collate``), so a whole
 test split is a handful of launch sequences.
 

@@ -15,7 +15,7 @@ _LIB_NAME = "libcgr_mpnn3d.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CGR_MPNN3D_LIB", os.path.join(_HERE, "lib", _LIB_NAME))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 TRAIN_DROPOUT, TRAIN_FOR_BACKWARD = 1, 2  # cgr_gnn_forward / _backward `training` bits
 MAX_DEPTH = 32
 ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
@@ -108,6 +108,7 @@ SIGNATURES = [
     ("cgr_profile_collect", c_int32, []),
     ("cgr_profile_reset", None, []),
     ("cgr_profile_report", c_int64, [c_char_p, c_int64]),
+    ("cgr_debug_stamps", c_int32, [c_void_p, c_int64]),
 ]
 
 _lib = None

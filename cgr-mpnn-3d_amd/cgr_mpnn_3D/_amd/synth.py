@@ -186,4 +186,8 @@ CONFIGS = {
                  learnable_skip=False),
     "cfg5": dict(num_graphs=512, n_atoms=30, n_bonds=30, n_mace=768, depth=6, hidden=512,
                  learnable_skip=True),
+    # what train.py users run: its defaults depth 3, hidden 300 (train.py:156-166) at its default
+    # batch size 32 (train.py:209), CGR + MACE features
+    "train_default": dict(num_graphs=32, n_atoms=30, n_bonds=30, n_mace=768, depth=3, hidden=300,
+                          learnable_skip=False),
 }

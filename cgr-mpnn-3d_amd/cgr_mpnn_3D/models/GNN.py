@@ -31,7 +31,7 @@ import torch.nn.functional as F
 
 from .._amd import config as _config
 from .._amd import native
-from .._amd.functional import ImageCache, gnn_forward, gnn_predict
+from .._amd.functional import gnn_forward, gnn_predict
 from .._amd.pool import global_add_pool, is_add_pool
 
 __all__ = ["GNN", "DMPNNConv", "global_add_pool"]
@@ -51,6 +51,27 @@ def _activation_code(fn) -> int:
     raise NotImplementedError(
         f"cgr_mpnn_3D (MI355X): activation_fn {fn!r} has no native kernel; supported are "
         "F.relu, F.silu, F.gelu (train.py:284-292)")
+
+
+def _warn_if_unpaired(edge_index):
+    """Once per module (its first forward; one device sync): warn when edge 2k+1 is not the
+    reverse of edge 2k.  The reference pairs e with e ^ 1 positionally whatever they hold
+    (flip(view(E/2, 2, H)), GNN.py:136-138) and so does the native path, so results stay exact;
+    but the CGR featuriser always emits (a, b), (b, a) pairs (graph_features.py:184-195), and
+    the fused layer backward's fast form relies on it -- unpaired input takes its grid-wide
+    last-workgroup form (ep_bwd.hpp), many times slower."""
+    import warnings
+
+    e = edge_index
+    if e.shape[1] < 2:
+        return
+    bad = (e[0, 1::2] != e[1, 0::2]) | (e[1, 1::2] != e[0, 0::2])
+    if bool(bad.any()):
+        warnings.warn(
+            "cgr_mpnn_3D: edge_index is not reverse-paired (edge 2k+1 is not the reverse of edge "
+            "2k, as the CGR featuriser emits them, graph_features.py:184-195); results follow "
+            "the reference's positional pairing exactly, but the native backward takes a slow "
+            "single-workgroup form", RuntimeWarning, stacklevel=3)
 
 
 class GNN(nn.Module):
@@ -107,8 +128,6 @@ class GNN(nn.Module):
         if not hasattr(self, "_cgr_instance"):
             GNN._cgr_instances += 1
             self._cgr_instance = GNN._cgr_instances
-        if not hasattr(self, "_cgr_images"):
-            self._cgr_images = ImageCache()  # forward weight images of the no-grad path
 
     def __setstate__(self, state):
         super().__setstate__(state)
@@ -202,6 +221,11 @@ class GNN(nn.Module):
             raise RuntimeError(
                 "Sizes of tensors must match: scatter size max(edge_index[1])+1 != num_nodes")
 
+        if not getattr(self, "_cgr_pairing_checked", False) and \
+                not torch.cuda.is_current_stream_capturing():
+            self._cgr_pairing_checked = True
+            _warn_if_unpaired(edge_index)
+
         params = self.native_parameters()
         for p in params:
             if p.dtype != torch.float32 or not p.is_cuda:
@@ -215,10 +239,9 @@ class GNN(nn.Module):
         params = [p.contiguous() for p in params]
         if not (torch.is_grad_enabled() and any(p.requires_grad for p in params)):
             # no gradient wanted (test.py / the CLI run under torch.no_grad()): the forward-only
-            # path, no saved activations, weight images cached across calls
+            # path, no saved activations
             return gnn_predict(cfg, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, drop,
-                               seed, training, [p.detach() for p in params], self._cgr_images,
-                               rng_counter=counter)
+                               seed, training, [p.detach() for p in params], rng_counter=counter)
         return gnn_forward(cfg, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, drop,
                            seed, training, params, self._grad_bucket_hook, rng_counter=counter)
 

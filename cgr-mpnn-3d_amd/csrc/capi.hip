@@ -146,6 +146,10 @@ ArenaLayout eval_arena_layout(const Dims& d) {
   }
   L.hn = b.take(4 * N * Hp);
   L.g = b.take(4 * B * Hp);
+  // forward weight images, packed by every predict that is not handed pre-packed ones
+  L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
+  L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
+  for (int l = 0; l < d.D; ++l) L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
   L.bytes = b.off;
   L.off_index_begin = 0;
   return L;
@@ -467,8 +471,8 @@ int cgr_gnn_predict(const cgr_gnn_config* cfg, const float* const* params, const
   if (rc) return rc;
   rc = validate_batch(cfg, b);
   if (rc) return rc;
-  CGR_CHECK(params != nullptr && images != nullptr && arena != nullptr && y != nullptr,
-            "cgr: params / images / arena / y must not be NULL");
+  CGR_CHECK(params != nullptr && arena != nullptr && y != nullptr,
+            "cgr: params / arena / y must not be NULL");
   CGR_CHECK((training & ~CGR_TRAIN_DROPOUT) == 0,
             "cgr_gnn_predict: `training` may only hold CGR_TRAIN_DROPOUT (no backward follows)");
   const int np = cgr_gnn_num_params(cfg);

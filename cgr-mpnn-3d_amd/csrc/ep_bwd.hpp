@@ -30,6 +30,7 @@
 
 #include "bwd_rows.hpp"
 #include "common.hpp"
+#include "stamps.hpp"
 
 namespace cgr {
 
@@ -124,6 +125,7 @@ struct EpLayerBwdSeg {
       }
       __syncthreads();
     }
+    CGR_STAMP(4);
     // rows of crossing segments (or every row, unpaired): raw dm[rev(r)]; all others: dh -> the
     // activation backward
     const int vh = sd[0] == sd[1] ? sd[0] : -3;               // head segment's node, if any
@@ -148,6 +150,7 @@ struct EpLayerBwdSeg {
       }
     }
 
+    CGR_STAMP(5);
     // ---- hand-off: the last contributor of a crossing segment (or of the grid) completes it ----
     const int tn = tile_id % tiles_n;
     float dsig_c[2] = {0.f, 0.f};  // learnable-skip partials of the segments completed here
@@ -229,6 +232,7 @@ struct EpLayerBwdSeg {
       }
     }
 
+    CGR_STAMP(6);
     // learnable-skip partials, at positions fixed by the data (not by which workgroup finished
     // last, so their fixed-order sum is deterministic): slot tile_id = this tile's rows; slot
     // gridDim.x + t = the rows of the crossing segment that STARTS in tile t (written by its

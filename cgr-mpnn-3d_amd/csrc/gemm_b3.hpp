@@ -34,6 +34,7 @@
 #include "epilogues.hpp"
 #include "gemm.hpp"
 #include "reduce.hpp"
+#include "stamps.hpp"
 
 namespace cgr {
 
@@ -209,6 +210,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   using S = B3NtShape<WAVES, RF, NF>;
   constexpr int NT = S::NT, BM = S::BM, BN = S::BN, BU4 = S::BU4, BPT = S::BPT;
   extern __shared__ b3_u4 b3_lds[];
+  CGR_STAMP_BEGIN();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
@@ -387,6 +389,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     storeB(b1, 1);
     splitA(a0, afr0, 0);
     __syncthreads();
+    CGR_STAMP(1);
     int cb = 0;  // LDS buffer of step ks (ks % 3)
     for (int ks = 0; ks < nk; ks += 2) {
       // even step: consume set 0 (A(ks+1), B(ks+2)), fill set 1 with A(ks+2), B(ks+3)
@@ -399,6 +402,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     }
   }
 
+  CGR_STAMP(2);
   // ---- epilogue (the stage buffers are dead after the last barrier) ----
   constexpr int C4 = BN / 4;
   constexpr int EIT = (BM * C4 + NT - 1) / NT;
@@ -429,6 +433,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       for (int r = 0; r < 4; ++r)
         C[((w * RF + i) * 16 + fg * 4 + r) * S::LDC + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
+  CGR_STAMP(3);
   if constexpr (TILE) {
     ep.template tile<BM, BN, NT, S::LDC, EIT>(pv, C, sd, m0, n0, tile, tid);
   } else {
@@ -444,6 +449,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         ep.apply4p(m0 + r, n0 + 4 * c4, *cp, pv[it], cx);
     }
   }
+  CGR_STAMP(4);
   if constexpr (SEG) {
     // a[v] = sum_{dst(i) = v} h[i] for the tile's columns (GNN.py:134): thread (16-row chunk,
     // float4 column) sums, in row order, every segment that STARTS in its chunk (running past
@@ -486,6 +492,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     }
   }
   }  // !TILE
+  CGR_STAMP_END((TILE ? 2 : 0) | (SEG ? 1 : 0) | (NF << 2) | (WAVES << 7));
 }
 
 template <int WAVES, int RF, int NF, bool NOMASK, class AL, class EP>

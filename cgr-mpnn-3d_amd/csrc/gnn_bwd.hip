@@ -22,6 +22,8 @@
 // forked right after its input is produced; every layer's dpre has a buffer of its own (the
 // edge-init backward sums them into dh0), so the main stream waits for the side stream only at
 // the very end.
+#include <string>
+
 #include "dispatch.hpp"
 #include "ep_bwd.hpp"
 #include "epilogues.hpp"
@@ -40,7 +42,10 @@ static hipError_t tn_gemm(const char* name, const AL& al, const BL& bl, int Nout
                           int target = kTnTargetWorkgroups) {
   *plan = tn_plan(Nout, Kout, R, target);
   const TnPlan p = *plan;
-  ProfScope _p(name, st);
+  // profile class "<name>[f32]": the fallback family is visible in the per-class report (tests
+  // assert which family ran for a width, bench.py keys its roofline on the plain names)
+  const std::string cls = std::string(name) + "[f32]";
+  ProfScope _p(cls.c_str(), st);
   return with_tn_shape(Nout, Kout, [&](auto W, auto RN) {
     return launch_tn<decltype(W)::value, decltype(RN)::value>(al, bl, p, slab, bslab,
                                                                          Nout, Kout, R, want_bias,
@@ -55,7 +60,8 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
                            hipStream_t st, int target = kTnrLayerTarget) {
   const TnrPlan q = plan_tnr<FA, FB>(Nout, Kout, R, target);
   *plan = TnPlan{q.tiles_n, q.tiles_k, q.splits, q.rows_per_split};
-  ProfScope _p(name, st);
+  const std::string cls = std::string(name) + "[tnr]";  // "<name>[tnr]", as tn_gemm's "[f32]"
+  ProfScope _p(cls.c_str(), st);
   return launch_gemm_tnr<FA, FB>(sa, sb, q, slab, bslab, Nout, Kout, R, want_bias, st);
 }
 

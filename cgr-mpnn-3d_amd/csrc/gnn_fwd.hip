@@ -75,7 +75,10 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   const ArenaLayout L = mode.eval ? eval_arena_layout(d) : arena_layout(d);
   const IndexView iv = index_view(arena, L);
   FloatView fv = float_view(arena, L, d);
-  if (mode.eval) {  // forward images from the caller (cgr_gnn_pack_images)
+  // forward weight images pre-packed by the caller (cgr_gnn_pack_images), or packed below into
+  // the arena by this call
+  const bool caller_images = mode.eval && mode.images != nullptr;
+  if (caller_images) {
     const ImageLayout IL = image_layout(d);
     char* im = static_cast<char*>(const_cast<void*>(mode.images));
     fv.b3x = d.F > 0 ? im + IL.b3x : nullptr;
@@ -128,7 +131,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   // layer / readout images (forward, and backward unless this is an eval forward) on the caller's
   // stream ahead of graph prep (that chain has slack beside the x-GEMM chain, and the layers
   // that read them run there)
-  if (F > 0 && !mode.eval) {
+  if (F > 0 && !caller_images) {
     ProfScope _p("weight_pack", side);
     B3PackJobs pj{};
     const B3Cols cx = b3_cols(2 * H);
@@ -138,13 +141,13 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
                                       H, F, cx.nimg, b3_nk(F)}, side));
     HIP_RET(b3_pack(pj, side));
   }
-  if (!mode.eval) {
+  if (!caller_images) {
     ProfScope _p("weight_pack", st);
     B3PackJobs pm{};
     HIP_RET(b3_pack_add(pm, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof), st));
     for (int l = 0; l < D; ++l)
       HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l]), st));
-    if (training & CGR_TRAIN_FOR_BACKWARD) {  // the backward NT GEMMs' W^T images
+    if (!mode.eval && (training & CGR_TRAIN_FOR_BACKWARD)) {  // the backward NT GEMMs' W^T images
       B3PackJob rob = b3_job(Wn + F, 1, F + H, H, H, fv.b3rob);  // scaled by wf: LdActGrad
       rob.kscale = params[CGR_PARAM_FFN_W(D)];
       HIP_RET(b3_pack_add(pm, rob, st));

@@ -129,8 +129,9 @@ int bwd_seg_tiles(const Dims& d);
 // the arena and the weight images are packed into it by each call.  Eval (cgr_gnn_predict): no
 // saved activations -- h_1.. h_D alias a two-buffer ring and a_0 .. a_D a three-buffer ring (the
 // fused layer epilogue zeroes the entries it accumulates two layers ahead, gnn_fwd.hip) -- and
-// the forward weight images come packed from the caller (cgr_gnn_pack_images), reused across
-// calls until the parameters change.
+// the forward weight images are packed into its arena by every call (the weights may have changed
+// by any route: an optimizer writing through raw pointers, a replayed captured step), unless the
+// caller hands pre-packed ones (cgr_gnn_pack_images) and vouches for their freshness.
 struct FwdMode {
   bool eval = false;
   const void* images = nullptr;

@@ -8,6 +8,7 @@
 
 #include "gnn_internal.hpp"
 #include "profiling.hpp"
+#include "stamps.hpp"
 
 namespace cgr {
 namespace {
@@ -55,6 +56,15 @@ void prof_end(void* token, hipStream_t st) {
   g_pending.push_back(r);
 }
 
+#ifdef CGR_STAMPS
+// setters of the per-translation-unit stamp buffer pointers (stamps.hpp)
+static std::vector<StampSetter>& stamp_setters() {
+  static std::vector<StampSetter> v;
+  return v;
+}
+void stamp_register(StampSetter f) { stamp_setters().push_back(f); }
+#endif
+
 }  // namespace cgr
 
 using namespace cgr;
@@ -101,6 +111,23 @@ int64_t cgr_profile_report(char* buf, int64_t len) {
     buf[n] = 0;
   }
   return (int64_t)s.size() + 1;
+}
+
+int cgr_debug_stamps(void* buffer, int64_t records) {
+#ifdef CGR_STAMPS
+  if (records < 0 || records > 0x7fffffff) {
+    set_error("cgr_debug_stamps: records out of range");
+    return CGR_ERR_INVALID_ARGUMENT;
+  }
+  for (StampSetter f : stamp_setters())
+    HIP_RET(f(static_cast<unsigned long long*>(buffer), (unsigned int)records));
+  return 0;
+#else
+  (void)buffer;
+  (void)records;
+  set_error("cgr_debug_stamps: not a stamp build (compile with -DCGR_STAMPS)");
+  return CGR_ERR_UNSUPPORTED;
+#endif
 }
 
 }  // extern "C"

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CGR_ABI_VERSION 3
+#define CGR_ABI_VERSION 4
 #define CGR_MAX_DEPTH 32
 
 enum cgr_status {
@@ -151,11 +151,13 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params,
 /* Forward-only inference (test.py:85-113 and cli_tool/activation_energy_predictor.py:70-80 run
  * GNN.forward under torch.no_grad() in eval mode).  cgr_gnn_predict computes exactly what
  * cgr_gnn_forward computes for `y`, but keeps no activation for a backward (h_1 .. h_D share a
- * two-buffer ring and a_0 .. a_D a three-buffer one: its arena is ~half the training arena) and
- * takes the split-bf16 forward weight images pre-packed by cgr_gnn_pack_images into `images`
- * (cgr_gnn_image_bytes bytes, caller-owned): pack once, predict many batches, re-pack only when
- * the parameters change.  `training` may only hold CGR_TRAIN_DROPOUT (module in train mode under
- * no_grad).  Sizes: cgr_gnn_predict_arena_bytes. */
+ * two-buffer ring and a_0 .. a_D a three-buffer one: its arena is ~half the training arena).
+ * `images` NULL: the split-bf16 forward weight images are packed from `params` into the arena by
+ * this call (one launch beside the graph bookkeeping; always current, whatever changed the weights
+ * -- an optimizer writing through raw pointers, a replayed captured step).  Non-NULL: images
+ * pre-packed by cgr_gnn_pack_images (cgr_gnn_image_bytes bytes, caller-owned), which the caller
+ * must re-pack whenever the parameters change.  `training` may only hold CGR_TRAIN_DROPOUT
+ * (module in train mode under no_grad).  Sizes: cgr_gnn_predict_arena_bytes. */
 int64_t cgr_gnn_image_bytes(const cgr_gnn_config* cfg);
 int cgr_gnn_pack_images(const cgr_gnn_config* cfg, const float* const* params, void* images,
                         void* stream);
@@ -249,6 +251,12 @@ int cgr_profile_enable(int32_t on);
 int cgr_profile_collect(void);
 void cgr_profile_reset(void);
 int64_t cgr_profile_report(char* buf, int64_t len);
+
+/* Diagnostic builds only (-DCGR_STAMPS, tools/stamp_lab.py): every split-bf16 NT GEMM workgroup
+ * appends one 16 x uint64 record of shader-clock phase stamps to `buffer` (device, zeroed by the
+ * caller; its first 16 bytes are the record counter) for at most `records` workgroups; NULL stops
+ * recording.  The product build returns CGR_ERR_UNSUPPORTED. */
+int cgr_debug_stamps(void* buffer, int64_t records);
 
 #ifdef __cplusplus
 }

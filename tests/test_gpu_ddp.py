@@ -7,12 +7,14 @@ soon as its event fires.  What is checked here, on one GPU:
     hook-free gradient, eagerly and inside a captured training step -- each event fired after its
     bucket's last write (an early event would let a later write overwrite the doubled values) and
     the buckets cover every parameter once;
-  * a world-1 RCCL process group (backend "nccl", in a child process of its own): the real
-    all_reduce(SUM) of every bucket inside a captured step leaves the gradients bitwise equal to
-    the run without the hook.
-The multi-rank arithmetic (sum of shard gradients == whole-batch gradient) is covered by
-tests/test_gpu_parity.py::test_cfg2_eight_shard_gradients_sum_to_whole_batch and, over gloo,
-tests/test_ddp.py.  Reference: the single-device step of train.py:109-114 / trainer.py:138-144.
+  * a world-1 RCCL process group (backend "nccl", in this process): the real all_reduce(SUM) of
+    every bucket inside a captured step leaves the gradients bitwise equal to the run without the
+    hook, and the process group is then torn down in the order ddp.teardown prescribes (captured
+    graphs first, then the communicator);
+  * two real ranks (two processes sharing the one GPU, gloo): each runs the native forward /
+    backward on its shard of the cfg2 batch with install_grad_allreduce; the all-reduced gradients
+    are bitwise identical on both ranks and equal the whole-batch native gradient (1e-4).
+Reference: the single-device step of train.py:109-114 / trainer.py:138-144.
 """
 
 import os
@@ -95,35 +97,86 @@ def _free_port():
     return port
 
 
-def _rccl_child():
-    """The world-1 RCCL case, run in a child process of its own: a fresh process (no GPU state
-    left by the tests before it) whose only exit is os._exit after the check -- the process group
-    is never destroyed there (RCCL's communicator teardown after a captured collective
-    intermittently aborted the pytest process, 2 of ~12 full-suite runs, after the test itself
-    had passed)."""
-    dev = torch.device("cuda:0")
-    m, data = _model(dev, D=4, H=400, skip=False)
+def test_world1_rccl_allreduce_inside_captured_step_is_bitwise_identity(cuda_device):
+    from cgr_mpnn_3D._amd.ddp import teardown
+
+    m, data = _model(cuda_device, D=4, H=400, skip=False)
     ref = _captured(m, data)
     store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
-    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=cuda_device)
+    try:
+        install_grad_allreduce(m)
+        eager = _grads(m, data)
+        cap = _captured(m, data)  # its graph (with the captured collectives) is gone on return
+        for a, c, r in zip(eager, cap, ref):
+            assert torch.equal(a, r)
+            assert torch.equal(c, r)
+    finally:
+        teardown(m)
+    assert not dist.is_initialized() and m._grad_bucket_hook is None
+
+
+def _two_rank_child(out_dir):
+    """One rank of the two-process run (RANK / WORLD_SIZE / MASTER_* from the parent)."""
+    import numpy as np
+
+    from cgr_mpnn_3D._amd.ddp import shard_batch, teardown
+    from cgr_mpnn_3D._amd.synth import CONFIGS
+
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = CONFIGS["cfg2"]
+    b = make_batch(c["num_graphs"], c["n_atoms"], c["n_bonds"], c["n_mace"], seed=1234)
+    D, H = c["depth"], c["hidden"]
+    torch.manual_seed(0)
+    m = GNN(b.x.shape[1], 14, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D).to(dev).train()
+    names = [k for k, _ in m.named_parameters()]
+    if rank == 0:  # the whole batch on one process, no hook: what the sum must equal
+        whole = _grads(m, b.to_torch(dev))
+        np.savez(os.path.join(out_dir, "whole.npz"),
+                 **{k: g.cpu().numpy() for k, g in zip(names, whole)})
     install_grad_allreduce(m)
-    eager = _grads(m, data)
-    cap = _captured(m, data)
-    ok = all(torch.equal(a, r) and torch.equal(c, r) for a, c, r in zip(eager, cap, ref))
+    reduced = _grads(m, shard_batch(b, rank, world).to_torch(dev))
     torch.cuda.synchronize()
-    print("RCCL_BITWISE_OK" if ok else "RCCL_MISMATCH", flush=True)
-    os._exit(0 if ok else 1)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"),
+             **{k: g.cpu().numpy() for k, g in zip(names, reduced)})
+    teardown(m)
+    print(f"RANK{rank}_OK", flush=True)
 
 
-def test_world1_rccl_allreduce_inside_captured_step_is_bitwise_identity(cuda_device):
+def test_two_ranks_on_one_gpu_allreduce_equals_whole_batch(cuda_device, tmp_path):
     import subprocess
-    import sys
 
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    r = subprocess.run([sys.executable, "-u", os.path.abspath(__file__), "--rccl-child"], env=env,
-                       capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "RCCL_BITWISE_OK" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
+    import numpy as np
+
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(r),
+                   WORLD_SIZE="2", LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen(
+            [sys.executable, "-u", os.path.abspath(__file__), "--two-rank", str(tmp_path)],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    for r, (p, o) in enumerate(zip(procs, outs)):
+        assert p.returncode == 0 and f"RANK{r}_OK" in o, o[-3000:]
+    whole = np.load(tmp_path / "whole.npz")
+    g0, g1 = np.load(tmp_path / "rank0.npz"), np.load(tmp_path / "rank1.npz")
+    for k in whole.files:
+        assert np.array_equal(g0[k], g1[k]), k  # every rank holds the same summed gradient
+        ref = whole[k].astype(np.float64)
+        err = np.abs(g0[k] - ref).max() / (np.abs(ref).max() + 1e-30)
+        assert err <= 1e-4, (k, err)
 
 
-if __name__ == "__main__" and "--rccl-child" in sys.argv:
-    _rccl_child()
+if __name__ == "__main__" and "--two-rank" in sys.argv:
+    _two_rank_child(sys.argv[sys.argv.index("--two-rank") + 1])

@@ -3,7 +3,7 @@
 GNN.forward takes it whenever no gradient is wanted -- test.py:100-113 and
 cli_tool/activation_energy_predictor.py:70-80 call the model under torch.no_grad() in eval mode.
 It runs the training forward's kernels in the same order, with h_1 .. h_D on a two-buffer ring,
-a_0 .. a_D on a three-buffer ring and weight images packed once per parameter version, so its
+a_0 .. a_D on a three-buffer ring and weight images packed into its own arena by every call, so its
 predictions must equal the training forward's bit for bit (and, through it, the reference goldens
 of test_gpu_parity.py, which also run under no_grad).
 """
@@ -74,31 +74,57 @@ def test_predict_cfg2_batch_vs_oracle_and_arena_size(cuda_device):
     assert 0 < pred < 0.7 * train  # (index bookkeeping, x copy and P / Q stay)
 
 
-def test_image_cache_follows_optimizer_updates(cuda_device):
+def _assert_predict_is_current(m, data):
+    m.eval()
+    with torch.no_grad():
+        y_pred = m(data)
+    y_train = m(data)  # grad-enabled forward: packs its images from the current weights
+    assert torch.equal(y_pred, y_train.detach())
+    m.train()
+
+
+@pytest.mark.parametrize("opt_kind", ["torch", "fused", "fused_captured"])
+def test_predict_follows_every_optimizer_update(opt_kind, cuda_device):
+    # a no-grad forward must see the weights after every optimizer step, however the
+    # step wrote them: torch.optim.Adam (in-place ops, version counters bump), the native
+    # FusedAdam (raw pointers: no version bump) and a captured training step replayed (nothing
+    # on the host changes at all) -- the reference trainer validates under no_grad after every
+    # epoch (trainer.py:167-170), test.py predicts from the trained weights
+    from cgr_mpnn_3D._amd.optim import FusedAdam
+
     b = make_batch(32, n_mace=32, seed=3)
     data = b.to_torch(cuda_device)
     m = _model(cuda_device, b.x.shape[1], 3, 128)
-    opt = torch.optim.Adam(m.parameters(), lr=1e-2)
-    for _ in range(2):
-        m.eval()
-        with torch.no_grad():
-            y_pred = m(data)
-        y_train = m(data)
-        assert torch.equal(y_pred, y_train.detach())  # images re-packed after every step
-        m.train()
-        opt.zero_grad()
+    opt = (torch.optim.Adam(m.parameters(), lr=1e-2, amsgrad=True) if opt_kind == "torch"
+           else FusedAdam(m.parameters(), lr=1e-2, amsgrad=True))
+    m.train()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
         torch.nn.MSELoss(reduction="sum")(m(data), data.y).backward()
         opt.step()
-    key = m._cgr_images.key
-    m.eval()
-    with torch.no_grad():
-        m(data)
-        m(data)
-    assert m._cgr_images.key != key  # the optimizer step changed the versions once...
-    key = m._cgr_images.key
-    with torch.no_grad():
-        m(data)
-    assert m._cgr_images.key == key  # ...and nothing re-packs without a change
+
+    _assert_predict_is_current(m, data)
+    if opt_kind != "fused_captured":
+        for _ in range(3):
+            step()
+            _assert_predict_is_current(m, data)
+        return
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    before = [p.detach().clone() for p in m.parameters()]
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        _assert_predict_is_current(m, data)
+    assert not all(torch.equal(a, p) for a, p in zip(before, m.parameters()))
 
 
 def test_predict_dropout_in_train_mode_under_no_grad(cuda_device):
