@@ -59,6 +59,8 @@ Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
   return d;
 }
 
+int bwd_seg_tiles(const Dims& d);
+
 namespace {
 struct Bump {
   size_t off = 0;
@@ -82,7 +84,11 @@ static void layout_prefix(const Dims& d, ArenaLayout& L, Bump& b) {
   L.cursor2 = L.cursor + 4 * N;
   L.graph_cnt = L.cursor2 + 4 * N;
   L.status = L.graph_cnt + 4 * B;
-  L.zero_bytes = (size_t)round_up((int64_t)(4 * (4 * N + B) + 16), 16);
+  // + the ticket counters of the layer GEMMs' hub segments (EpLayerSeg: zero on entry, reset by
+  // each completer)
+  L.fcnt = L.status + 16;
+  const size_t fcnt_n = N * (size_t)b3_cols(d.H).tiles;
+  L.zero_bytes = (size_t)round_up((int64_t)(4 * (4 * N + B) + 16 + 4 * fcnt_n), 16);
   b.take(L.zero_bytes);
   L.rng = b.take(8);
   L.perm = b.take(4 * E);
@@ -102,6 +108,8 @@ static void layout_prefix(const Dims& d, ArenaLayout& L, Bump& b) {
   L.P = b.take(4 * N * Hp);
   L.Q = b.take(4 * N * Hp);
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
+  // partial sums of the layer GEMMs' hub segments (over >= 3 row tiles), one slot pair per tile
+  L.fpart = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)b3_cols(d.H).nf * 16);
 }
 
 ArenaLayout arena_layout(const Dims& d) {
@@ -177,6 +185,8 @@ IndexView index_view(void* arena, const ArenaLayout& L) {
   v.cursor2 = (int*)at(arena, L.cursor2);
   v.graph_cnt = (int*)at(arena, L.graph_cnt);
   v.status = (int*)at(arena, L.status);
+  v.fcnt = (int*)at(arena, L.fcnt);
+  v.fpart = (float*)at(arena, L.fpart);
   v.rng = (uint64_t*)at(arena, L.rng);
   v.zero_block = at(arena, L.zero_block);
   v.zero_bytes = L.zero_bytes;
@@ -282,6 +292,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.bslab2 = b.take(4 * std::max<size_t>(bslab, 1));
   W.dag = b.take(2 * 4 * N * Hp);  // two, alternating by layer
   W.cnt = b.take(4 * (N * (size_t)b3_cols(d.H).tiles + 1));
+  W.part = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)b3_cols(d.H).nf * 16);
   W.dsig_blocks = bwd_dsig_slots(d);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
   W.bytes = b.off;

@@ -15,8 +15,11 @@
 //
 // Segments crossing a row-tile boundary (at most one at each end of a tile) are completed inside
 // the launch by the LAST of their contributing workgroups (cdna_hip_programming.md §6
-// Guideline 16, counter form): each contributor adds its partial sum atomically to `dag` (two
-// contributors: order-independent, so deterministic for in-degrees <= rows per tile + 1) and
+// Guideline 16, counter form): each contributor hands over its partial sum -- a segment over two
+// row tiles adds it atomically to `dag` (two addends onto zero: order-independent), one over
+// three or more (a hub node: in-degree > rows per tile + 1) stores it write-through into a slot
+// fixed by the data (`part`, slot_of below), which the completer sums in row-tile order, so every
+// reduction is deterministic whatever the in-degree -- and
 // stores the segment's raw rows write-through (sc1), publishes them (vmcnt drain, barrier: no
 // release fence -- an agent-scope release writes back the XCD's L2, here full of the dpre rows
 // just stored: the fenced form ran each GEMM 15-20 us longer) and draws a ticket from the
@@ -30,27 +33,10 @@
 
 #include "bwd_rows.hpp"
 #include "common.hpp"
+#include "handoff.hpp"
 #include "stamps.hpp"
 
 namespace cgr {
-
-__device__ __forceinline__ void ep_vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// handed-off words (Guideline 16 R1): agent-scope relaxed atomic stores / loads are the sc1
-// (write-through / L2-bypassing) forms, so the hand-off needs no release or acquire fence
-__device__ __forceinline__ void sc1_store4(float* p, float4 v) {
-  __hip_atomic_store(p, v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(p + 1, v.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(p + 2, v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(p + 3, v.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float4 sc1_load4(const float* p) {
-  float* q = const_cast<float*>(p);
-  return make_float4(__hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                     __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                     __hip_atomic_load(q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                     __hip_atomic_load(q + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
 
 template <bool EDGE_INIT>
 struct EpLayerBwdSeg {
@@ -64,6 +50,7 @@ struct EpLayerBwdSeg {
   const int* src_ptr;
   float* dag;          // [nodes, Hp] crossing-segment partial sums of da (zero on entry)
   float* dag_next;     // the next layer's (or null): completed segments' entries zeroed
+  float* part;         // [tiles, 2, BN] partials of segments over >= 3 row tiles (slot_of)
   int* cnt;            // [nodes * tiles_n + 1] tickets (zero on entry, left zero)
   const int* status;   // graph prep's status word
   int M, N, nodes, tiles_n;
@@ -109,11 +96,17 @@ struct EpLayerBwdSeg {
             da = f4add(da, *reinterpret_cast<const float4*>(&C[r * LDC + 4 * c4]));
           const bool head = s == 0 && sd[0] == v, tail = r == nrow && sd[nrow + 1] == v;
           if (head || tail) {
-            float* g = dag + (int64_t)v * a.Hp + col;
-            atomicAdd(g, da.x);
-            atomicAdd(g + 1, da.y);
-            atomicAdd(g + 2, da.z);
-            atomicAdd(g + 3, da.w);
+            const int b = dst_ptr[v], e = dst_ptr[v + 1];
+            if (seg_tiles(b, e, BM) <= 2) {
+              float* g = dag + (int64_t)v * a.Hp + col;
+              atomicAdd(g, da.x);
+              atomicAdd(g + 1, da.y);
+              atomicAdd(g + 2, da.z);
+              atomicAdd(g + 3, da.w);
+            } else {
+              const int slot = slot_of(m0 / BM, b / BM);
+              sc1_store4(part + ((int64_t)tile_id * 2 + slot) * BN + 4 * c4, da);
+            }
           } else {
             for (int k = s; k < r; ++k) {
               float4* cp = reinterpret_cast<float4*>(&C[k * LDC + 4 * c4]);
@@ -198,10 +191,27 @@ struct EpLayerBwdSeg {
           const int64_t gv = (int64_t)v * a.Hp;
           float ds = 0.f;
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the ticket
+          // da of the segment per column into LDS (the tile's accumulators are dead): the atomic
+          // sum of two partials, or the slots of every row tile in row order
+          const int t0 = ib / BM, t1 = (ie - 1) / BM;
+          float4* das = reinterpret_cast<float4*>(C);
+          __syncthreads();  // previous segment's das reads done
+          for (int c4 = tid; c4 < C4; c4 += NT) {
+            float4 da = f4zero();
+            if (t1 - t0 + 1 <= 2) {
+              da = sc1_load4(dag + gv + n0 + 4 * c4);
+            } else {
+              for (int t = t0; t <= t1; ++t)
+                da = f4add(da, sc1_load4(part + ((int64_t)(t * tiles_n + tn) * 2 + slot_of(t, t0)) *
+                                                    BN + 4 * c4));
+            }
+            das[c4] = da;
+          }
+          __syncthreads();
           for (int q = tid; q < (ie - ib) * C4; q += NT) {
             const int i = ib + q / C4, col = n0 + 4 * (q % C4);
             if (col >= N) continue;
-            const float4 da = sc1_load4(dag + gv + col);
+            const float4 da = das[q % C4];
             const float4 x = sc1_load4(raw + (int64_t)i * a.Hp + col);
             bwd_row_apply<EDGE_INIT>(a, i, col, f4sub(da, x), key, ds,
                                      bwd_row_loads<EDGE_INIT>(a, i, col));

@@ -148,6 +148,12 @@ struct EpLayerSeg : EpLayer {
   float* aout;       // [nodes, lda]; crossing / empty segments zeroed beforehand
   int64_t lda;
   float* znext;      // or null: [nodes, lda] whose crossing segments this GEMM zeroes (eval ring)
+  // hub segments (over >= 3 row tiles: in-degree > rows per tile + 1), completed in fixed order
+  // by their last contributor (gemm_b3nt_kernel, handoff.hpp)
+  const int* dst_ptr;  // [nodes + 1] dst CSR of the sorted rows
+  float* part;         // [tiles, 2, BN] their partial sums (slot_of)
+  int* cnt;            // [nodes * tiles_n] tickets (zero on entry, left zero)
+  int tiles_n;
   // apply4p that also returns the stored h (rows / columns outside: v unchanged)
   __device__ __forceinline__ float4 apply4p_h(int r, int c, float4 v, const Pre& p,
                                               const Ctx& cx) const {

@@ -33,6 +33,7 @@
 
 #include "epilogues.hpp"
 #include "gemm.hpp"
+#include "handoff.hpp"
 #include "reduce.hpp"
 #include "stamps.hpp"
 
@@ -454,10 +455,11 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     // a[v] = sum_{dst(i) = v} h[i] for the tile's columns (GNN.py:134): thread (16-row chunk,
     // float4 column) sums, in row order, every segment that STARTS in its chunk (running past
     // the chunk's end as needed), and the chunk-0 thread also the head segment begun in the
-    // previous tile.  A segment inside the tile is stored; one crossing a tile boundary is added
-    // atomically to a[v], which edge_init_segsum_fwd zeroed: with the two partials of a segment
-    // that spans two tiles the sum is order-independent (p + q == q + p), so the result is
-    // deterministic for every node of in-degree <= BM + 1.
+    // previous tile.  A segment inside the tile is stored; one crossing into one neighbouring
+    // tile is added atomically to a[v], which edge_init_segsum_fwd zeroed (two partials onto
+    // zero: p + q == q + p, deterministic); one over three or more row tiles (a hub node,
+    // in-degree > BM + 1) leaves its partial in a slot fixed by the data and its last
+    // contributor sums the slots in row-tile order -- deterministic for every in-degree.
     __syncthreads();
     const int nrow = min(BM, M - m0);
     constexpr int NCH = BM / 16;
@@ -480,14 +482,62 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         if (tail && !head && ep.znext)  // the tile where a crossing segment starts
           *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + col) = f4zero();
         if (head || tail) {
-          atomicAdd(dst, a.x);
-          atomicAdd(dst + 1, a.y);
-          atomicAdd(dst + 2, a.z);
-          atomicAdd(dst + 3, a.w);
+          const int b = ep.dst_ptr[v], e = ep.dst_ptr[v + 1];
+          if (seg_tiles(b, e, BM) <= 2) {
+            atomicAdd(dst, a.x);
+            atomicAdd(dst + 1, a.y);
+            atomicAdd(dst + 2, a.z);
+            atomicAdd(dst + 3, a.w);
+          } else {
+            sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * c4, a);
+          }
         } else {
           *reinterpret_cast<float4*>(dst) = a;
         }
         s = r;
+      }
+    }
+    // hub segments: the last contributor sums the slots of every row tile in order
+    const int vh = sd[0] == sd[1] ? sd[0] : -3;               // head segment's node, if any
+    const int vt = sd[nrow] == sd[nrow + 1] ? sd[nrow] : -3;  // tail segment's node, if any
+    auto hub = [&](int v) {
+      return v >= 0 && seg_tiles(ep.dst_ptr[v], ep.dst_ptr[v + 1], BM) >= 3;
+    };
+    const bool bh = hub(vh), bt = vt != vh && hub(vt);  // uniform over the workgroup
+    if (bh || bt) {
+      int* scratch = sd + BM + 2;  // 16 words (B3NtShape::EPI_BYTES)
+      ep_vm_drain();  // this wave's slot stores
+      __syncthreads();
+      if (tid == 0) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int v = k == 0 ? (bh ? vh : -3) : (bt ? vt : -3);
+          int done = 0;
+          if (v >= 0) {
+            const int cnt = seg_tiles(ep.dst_ptr[v], ep.dst_ptr[v + 1], BM);
+            done = __hip_atomic_fetch_add(&ep.cnt[(int64_t)v * ep.tiles_n + tn], 1,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == cnt - 1;
+          }
+          scratch[14 + k] = done ? v : -1;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int v = scratch[14 + k];
+        if (v < 0) continue;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the ticket
+        const int t0 = ep.dst_ptr[v] / BM, t1 = (ep.dst_ptr[v + 1] - 1) / BM;
+        for (int c4 = tid; c4 < C4; c4 += NT) {
+          const int col = n0 + 4 * c4;
+          if (col >= ep.N) continue;
+          float4 a = f4zero();
+          for (int t = t0; t <= t1; ++t)
+            a = f4add(a, sc1_load4(ep.part + ((int64_t)(t * tiles_n + tn) * 2 + slot_of(t, t0)) *
+                                                 BN + 4 * c4));
+          *reinterpret_cast<float4*>(ep.aout + (int64_t)v * ep.lda + col) = a;
+        }
+        if (tid == 0) ep.cnt[(int64_t)v * ep.tiles_n + tn] = 0;
       }
     }
   }
@@ -501,7 +551,8 @@ inline hipError_t launch_b3nt_t(const AL& al, const b3_u4* Bimg, int nimg, const
   using S = B3NtShape<WAVES, RF, NF>;
   auto kern = gemm_b3nt_kernel<WAVES, RF, NF, NOMASK, AL, EP>;
   static LdsLimit lim;
-  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), 160 * 1024);
+  // the dynamic bytes this launch asks for (a diagnostic build adds static LDS: stamps.hpp)
+  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), (int)S::LDS_BYTES);
   if (e != hipSuccess) return e;
   const int tm = (M + S::BM - 1) / S::BM;
   hipLaunchKernelGGL(kern, dim3(tm * tiles_n), dim3(WAVES * 64), S::LDS_BYTES, st, al, Bimg, nimg,
@@ -777,12 +828,6 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int h = 0; h < TB::NL / 8; ++h) off[8 * h + j] = TB::off(bl, ix[j], h, gcol, Kout);
-#ifdef CGR_TNI_LAB
-      if (CGR_TNI_LAB & 1) {
-        for (int i = 0; i < 16; ++i) raw[i] = make_float4(off[i & (TB::NL - 1)] * 1e-9f, 1.f, 2.f, 3.f);
-        return;
-      }
-#endif
 #pragma unroll
       for (int i = 0; i < 4; ++i) raw[i] = *reinterpret_cast<const float4*>(base0 + off[i]);
       if constexpr (TB::NL == 16) {
@@ -803,12 +848,6 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
     };
     auto stage = [&](const float4 (&raw)[16], int buf) {
       b3_u4* img = b3_lds + buf * SU4;
-#ifdef CGR_TNI_LAB
-      if (CGR_TNI_LAB & 8) {
-        if (raw[0].x == 123.f) img[tid] = b3_u4{1, 2, 3, 4};
-        return;
-      }
-#endif
       float4 u[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) u[j] = TB::get(raw, j);
@@ -869,12 +908,6 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
   for (int f = 0; f < NA; ++f) bsum[f] = 0.f;
   const int s0 = e_begin / 32;
   auto aload = [&](int t, b3_u4 (&a)[NA][2]) {
-#ifdef CGR_TNI_LAB
-    if (CGR_TNI_LAB & 2) {
-      for (int f = 0; f < NA; ++f) a[f][0] = a[f][1] = b3_u4{(uint32_t)t, 1u, 2u, 3u};
-      return;
-    }
-#endif
     const int s = s0 + (t < nt ? t : nt - 1);
     const b3_u4* base = ai.img + (size_t)s * 2 * ai.cimg * 4;
 #pragma unroll
@@ -893,12 +926,6 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
   for (int x = 0; x < RX; ++x) accx[x] = floatx4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int buf, const b3_u4 (&a)[NA][2]) {
     const b3_u4* img = b3_lds + buf * SU4;
-#ifdef CGR_TNI_LAB
-    if (CGR_TNI_LAB & 4) {
-      acc[0][0][0] += (float)img[sw].x + (float)a[0][0].x;
-      return;
-    }
-#endif
 #pragma unroll
     for (int x = 0; x < RX; ++x) {
       const int rb = (xq(x) % TNK) * 16 + rrow;

@@ -293,6 +293,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   const int seg_cols = b3_cols(H).tiles;
   const int seg_tiles = bwd_seg_tiles(d);
   int* cnt = reinterpret_cast<int*>(ws + WL.cnt);
+  float* part = reinterpret_cast<float*>(ws + WL.part);
   auto layer_args = [&](int l) {
     uint32_t thresh;
     float scale;
@@ -368,13 +369,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       if (l > 0)
         HIP_RET(launch_b3nt(al, img,
                             EpLayerBwdSeg<false>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
-                                                 iv.src_ptr, dg, dgn, cnt, iv.status, E, H, N,
+                                                 iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
                                                  seg_cols},
                             E, H, H, st));
       else
         HIP_RET(launch_b3nt(al, img,
                             EpLayerBwdSeg<true>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
-                                                iv.src_ptr, dg, dgn, cnt, iv.status, E, H, N,
+                                                iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
                                                 seg_cols},
                             E, H, H, st));
     }

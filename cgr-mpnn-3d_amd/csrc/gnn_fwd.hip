@@ -229,8 +229,10 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       // eval ring: a_{l+2} reuses a_{l-1}'s buffer, free once layer l-1 read it; this layer
       // zeroes the entries layer l+1 will accumulate there
       float* znext = (mode.eval && l >= 1 && l + 2 <= D) ? fv.a[l + 2] : nullptr;
-      HIP_RET(launch_b3nt(al, img, EpLayerSeg{ep, iv.dst_s, fv.a[l + 1], Hp, znext}, E, H, H,
-                          st));
+      HIP_RET(launch_b3nt(al, img,
+                          EpLayerSeg{ep, iv.dst_s, fv.a[l + 1], Hp, znext, iv.dst_ptr, iv.fpart,
+                                     iv.fcnt, b3_cols(H).tiles},
+                          E, H, H, st));
     } else {
       {
         ProfScope _p("gemm_nt_layer_fwd", st);

@@ -47,6 +47,8 @@ struct IndexView {
   int* cursor2;
   int* graph_cnt;
   int* status;
+  int* fcnt;     // [N * column tiles] hub-segment tickets of the layer GEMMs (in the zero block)
+  float* fpart;  // [tiles, 2, BN] hub-segment partial sums of the layer GEMMs
   uint64_t* rng;  // effective dropout key of this forward (read by every dropout kernel)
   void* zero_block;
   size_t zero_bytes;
@@ -97,6 +99,7 @@ struct ArenaLayout {
   size_t bytes;
   // offsets (bytes) for every buffer
   size_t zero_block, zero_bytes, deg_dst, deg_src, cursor, cursor2, graph_cnt, status, rng;
+  size_t fcnt, fpart;
   size_t perm, src_s, dst_s, rev_s, src_list, inv, src_c, dst_c, dst_ptr, src_ptr, graph_ptr,
       node_graph;
   size_t e_s, w0eT, P, Q, xp, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1],
@@ -120,6 +123,8 @@ struct WorkspaceLayout {
   size_t dag;
   // [N * column tiles + 1] ticket counters of those segments (and of the grid, unpaired form)
   size_t cnt;
+  // [row tiles * column tiles, 2, BN] partial sums of the segments over >= 3 row tiles
+  size_t part;
   int dsig_blocks;
 };
 int bwd_dsig_slots(const Dims& d);

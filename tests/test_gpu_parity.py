@@ -602,6 +602,22 @@ def test_cuda_graph_capture_replays_fwd_bwd(cuda_device):
         assert torch.equal(a, c)
 
 
+class _WarnCount:
+    """Counts the 'not reverse-paired' RuntimeWarnings raised inside the block."""
+
+    def __enter__(self):
+        import warnings
+
+        self._cm = warnings.catch_warnings(record=True)
+        self._rec = self._cm.__enter__()
+        warnings.simplefilter("always")
+        return self
+
+    def __exit__(self, *exc):
+        self.count = sum("reverse-paired" in str(w.message) for w in self._rec)
+        return self._cm.__exit__(*exc)
+
+
 def _sparse_batch(num_graphs, n_atoms, seed):
     """Reactions whose atoms are mostly unbonded: per graph a 3-bond chain 0-1-2-3 plus a bond
     from atom 0 to the last atom (the reference needs the batch's last node to have an incoming
@@ -655,6 +671,14 @@ def test_unpaired_edge_order_vs_oracle(act, skip, cuda_device):
     assert _pair_status(b, cuda_device) == 0
     assert _pair_status(u, cuda_device) == 4
     _oracle_compare(u, 64, 3, act, skip, cuda_device)
+    # a model warns once (its first forward) when the edge order is not reverse-paired
+    torch.manual_seed(0)
+    for batch, n_warn in ((b, 0), (u, 1)):
+        m = GNN(b.x.shape[1], 14, depth=1, hidden_sizes=[16], dropout_ps=[0.0]).to(cuda_device)
+        with _WarnCount() as wc:
+            m(batch.to_torch(cuda_device))
+            m(batch.to_torch(cuda_device))
+        assert wc.count == n_warn
 
 
 @pytest.mark.parametrize("act,skip", [("relu", True), ("silu", True), ("relu", False)])
@@ -714,12 +738,33 @@ def _hub_batch(leaves, seed):
                     ptr=np.array(ptr, np.int64), y=y)
 
 
+def _assert_bitwise_reruns(b, H, D, skip, dev, runs=3):
+    # hub segments over >= 3 row tiles are summed from data-determined slots in row-tile order
+    # (handoff.hpp): the forward (training and predict paths) and every gradient must repeat bit
+    # for bit, whichever workgroup happens to finish last
+    torch.manual_seed(5)
+    m = GNN(b.x.shape[1], b.edge_attr.shape[1], depth=D, hidden_sizes=[H] * D,
+            dropout_ps=[0.0] * D, use_learnable_skip=skip).to(dev).train()
+    data = b.to_torch(dev)
+    y0, g0 = _run(m, data)
+    with torch.no_grad():
+        p0 = m(data)
+    for _ in range(runs - 1):
+        y, g = _run(m, data)
+        assert torch.equal(y, y0)
+        for k in g0:
+            assert torch.equal(g[k], g0[k]), k
+        with torch.no_grad():
+            assert torch.equal(m(data), p0)
+
+
 @pytest.mark.parametrize("skip", [True, False])
 def test_hub_segments_spanning_tiles_vs_oracle(skip, cuda_device):
     # 64-row tiles (few workgroups): hub in-degrees 150 / 70 / 300 span 3-6 tiles
     b = _hub_batch([150, 3, 70, 300, 5], seed=41)
     assert _pair_status(b, cuda_device) == 0
     _oracle_compare(b, 64, 3, "relu", skip, cuda_device)
+    _assert_bitwise_reruns(b, 64, 3, skip, cuda_device)
 
 
 def test_hub_segments_spanning_128_row_tiles_vs_oracle(cuda_device):
@@ -727,6 +772,7 @@ def test_hub_segments_spanning_128_row_tiles_vs_oracle(cuda_device):
     b = _hub_batch([130 + (37 * g) % 271 for g in range(48)], seed=42)
     assert b.edge_index.shape[1] >= 96 * 128
     _oracle_compare(b, 48, 2, "relu", True, cuda_device)
+    _assert_bitwise_reruns(b, 48, 2, True, cuda_device)
 
 
 def test_unpaired_edge_order_128_row_tiles_vs_oracle(cuda_device):

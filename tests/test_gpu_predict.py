@@ -71,7 +71,9 @@ def test_predict_cfg2_batch_vs_oracle_and_arena_size(cuda_device):
     N, E, B = b.x.shape[0], b.edge_index.shape[1], b.num_graphs
     train = lib.cgr_gnn_arena_bytes(ctypes.byref(cfg), N, E, B)
     pred = lib.cgr_gnn_predict_arena_bytes(ctypes.byref(cfg), N, E, B)
-    assert 0 < pred < 0.7 * train  # (index bookkeeping, x copy and P / Q stay)
+    images = lib.cgr_gnn_image_bytes(ctypes.byref(cfg))  # packed into the predict arena per call
+    assert 0 < images < pred
+    assert pred - images < 0.7 * train  # (index bookkeeping, x copy and P / Q stay)
 
 
 def _assert_predict_is_current(m, data):

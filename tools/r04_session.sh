@@ -43,3 +43,8 @@ if [ "${SKIP_GLOO:-0}" = "0" ]; then
   echo "gloo2 rc=$rc"; tail -c 600 "$OUT/bench_gloo2.json"; fatal $rc && exit 1
 fi
 st done
+if [ "${PROBE:-0}" = "1" ]; then
+  st "rccl teardown probe"
+  AMD_LOG_LEVEL=${PROBE_LOG:-1} timeout -k 10 240 python -u tools/rccl_teardown_probe.py > "$OUT/probe.log" 2>&1; rc=$?
+  echo "probe rc=$rc"; grep -v "^Extension modules" "$OUT/probe.log" | tail -40
+fi
