@@ -18,6 +18,8 @@ per-rank gradients reproduces the single-process gradient of the whole global ba
 
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -98,6 +100,29 @@ def remove_grad_allreduce(model):
     return model
 
 
+def _collect_verbosely():
+    """Diagnostic (CGR_TEARDOWN_DIAG=1): free the collector's garbage one object at a time,
+    naming each on stderr first, so an abort inside the collection names its object."""
+    import gc
+    import sys
+
+    gc.set_debug(gc.DEBUG_SAVEALL)
+    gc.collect()
+    gc.set_debug(0)
+    junk = list(gc.garbage)
+    gc.garbage.clear()
+    print(f"[teardown] {len(junk)} collectable objects", file=sys.stderr, flush=True)
+    while junk:
+        o = junk.pop()
+        t = type(o)
+        if "torch" in t.__module__ or "cgr" in t.__module__ or t.__name__ in ("Event", "Stream"):
+            print(f"[teardown] freeing {t.__module__}.{t.__qualname__}", file=sys.stderr,
+                  flush=True)
+        del o
+        gc.collect()
+    print("[teardown] garbage freed", file=sys.stderr, flush=True)
+
+
 def teardown(model=None):
     """End data parallelism in the order the communicator needs, then destroy the process group.
 
@@ -118,6 +143,8 @@ def teardown(model=None):
         return
     if torch.cuda.is_available():
         torch.cuda.synchronize()
+    if os.environ.get("CGR_TEARDOWN_DIAG") == "1":
+        _collect_verbosely()
     gc.collect()
     if torch.cuda.is_available():
         torch.cuda.synchronize()

@@ -100,6 +100,10 @@ def _free_port():
 def test_world1_rccl_allreduce_inside_captured_step_is_bitwise_identity(cuda_device):
     from cgr_mpnn_3D._amd.ddp import teardown
 
+    import gc
+
+    gc.collect()  # what earlier tests left in reference cycles goes before the communicator exists
+    torch.cuda.synchronize()
     m, data = _model(cuda_device, D=4, H=400, skip=False)
     ref = _captured(m, data)
     store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)

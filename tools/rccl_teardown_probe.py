@@ -64,9 +64,9 @@ def main():
     # free in stages: tensors first, then everything else
     tens = [o for o in gc.garbage if isinstance(o, torch.Tensor)]
     say("freeing", len(tens), "tensors")
-    for o in tens:
-        gc.garbage.remove(o)
-    del tens, o
+    for t in tens:
+        gc.garbage.remove(t)
+    del tens
     gc.collect()
     torch.cuda.synchronize()
     say("tensors freed; freeing the rest:", len(gc.garbage))
