@@ -29,11 +29,15 @@ __device__ __forceinline__ RowOps layer_row_loads(const LayerBwdArgs& a, int64_t
   return r;
 }
 
+// A >= 0: the activation as a compile-time constant (one straight-line path per activation, no
+// per-element branch tree); A < 0: a.act at run time
+template <int A = -1>
 __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
                                                 uint64_t key, float& dsig, const RowOps& r) {
+  const int act = A < 0 ? a.act : A;
   const int64_t o = i * a.Hp + n;
   float d[4] = {dh.x, dh.y, dh.z, dh.w};
-  if (a.act == ACT_RELU) {  // h_{l+1} > 0 <=> relu active and kept by dropout
+  if (act == ACT_RELU) {  // h_{l+1} > 0 <=> relu active and kept by dropout
     const float hh[4] = {r.m.x, r.m.y, r.m.z, r.m.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
@@ -45,7 +49,7 @@ __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i
       if (a.thresh && n + k < a.H)
         m = drop_keep(key, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
                                                                                       : 0.f;
-      d[k] = d[k] * m * act_grad(zz[k], a.act);
+      d[k] = d[k] * m * act_grad(zz[k], act);
     }
   }
   const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
@@ -76,20 +80,22 @@ __device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t 
   return r;
 }
 
+template <int A = -1>
 __device__ __forceinline__ void edge_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
                                                const RowOps& r) {
+  const int act = A < 0 ? a.act : A;
   const int64_t o = i * a.Hp + n;
   float4 d = f4add(r.acc, dh);
-  if (a.act == ACT_RELU) {
+  if (act == ACT_RELU) {
     d.x = r.m.x > 0.f ? d.x : 0.f;
     d.y = r.m.y > 0.f ? d.y : 0.f;
     d.z = r.m.z > 0.f ? d.z : 0.f;
     d.w = r.m.w > 0.f ? d.w : 0.f;
   } else {
-    d.x *= act_grad(r.m.x, a.act);
-    d.y *= act_grad(r.m.y, a.act);
-    d.z *= act_grad(r.m.z, a.act);
-    d.w *= act_grad(r.m.w, a.act);
+    d.x *= act_grad(r.m.x, act);
+    d.y *= act_grad(r.m.y, act);
+    d.z *= act_grad(r.m.z, act);
+    d.w *= act_grad(r.m.w, act);
   }
   *reinterpret_cast<float4*>(a.dpre + o) = d;
 }
@@ -100,11 +106,11 @@ __device__ __forceinline__ RowOps bwd_row_loads(const LayerBwdArgs& a, int64_t i
   if constexpr (EDGE_INIT) return edge_row_loads(a, i, n);
   else return layer_row_loads(a, i, n);
 }
-template <bool EDGE_INIT>
+template <bool EDGE_INIT, int A = -1>
 __device__ __forceinline__ void bwd_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
                                               uint64_t key, float& dsig, const RowOps& r) {
-  if constexpr (EDGE_INIT) edge_row_apply(a, i, n, dh, r);
-  else layer_row_apply(a, i, n, dh, key, dsig, r);
+  if constexpr (EDGE_INIT) edge_row_apply<A>(a, i, n, dh, r);
+  else layer_row_apply<A>(a, i, n, dh, key, dsig, r);
 }
 
 }  // namespace cgr

@@ -31,6 +31,8 @@
 // nodes (correct, slow: a single workgroup -- the CGR edge order is always paired).
 #pragma once
 
+#include <type_traits>
+
 #include "bwd_rows.hpp"
 #include "common.hpp"
 #include "handoff.hpp"
@@ -56,7 +58,8 @@ struct EpLayerBwdSeg {
   int M, N, nodes, tiles_n;
 
   struct Ctx {};
-  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
+  __device__ __forceinline__ void finish_ctx(Ctx&) const {}
   typedef RowOps Pre;
   // operands of row r, columns c..c+3 (unconditional loads from clamped in-bounds addresses)
   __device__ __forceinline__ Pre pre4(int r, int c) const {
@@ -67,23 +70,34 @@ struct EpLayerBwdSeg {
 
   // C: the tile's accumulators [BM][LDC] in LDS (column j of the tile = output column n0 + j);
   // sd[q]: dst of rows m0 - 1 + q (q < BM + 2; distinct negative sentinels outside [0, M)),
-  // followed by 16 words of scratch; pv: pre4 of the items (r, c4) = (q / C4, q % C4),
-  // q = tid + it * NT; tile_id: this workgroup's tile (tm * tiles_n + tn)
-  template <int BM, int BN, int NT, int LDC, int EIT>
+  // followed by 16 words of scratch; thread tid < RPP * C4 owns the float4 column group
+  // tid % C4 of rows tid / C4 + RPP * it, and pv[it] holds pre4 of those pieces;
+  // tile_id: this workgroup's tile (tm * tiles_n + tn)
+  template <int BM, int BN, int NT, int LDC, int EIT, int RPP>
   __device__ __forceinline__ void tile(const Pre (&pv)[EIT], float* C, const int* sd, int m0,
                                        int n0, int tile_id, int tid) const {
-    constexpr int C4 = BN / 4, NCH = BM / 16;
+    constexpr int C4 = BN / 4;
+    const bool eact = tid < RPP * C4;
+    const int ec4 = eact ? tid % C4 : 0, er0 = tid / C4;
+    const int col = n0 + 4 * ec4;
     const int nrow = min(BM, M - m0);
     const bool paired = (*status & 4) == 0;
     int* scratch = const_cast<int*>(sd) + BM + 2;  // 16 words
+    const int vh = sd[0] == sd[1] ? sd[0] : -3;               // head segment's node, if any
+    const int vt = sd[nrow] == sd[nrow + 1] ? sd[nrow] : -3;  // tail segment's node, if any
+    const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
+    float dsig = 0.f;
     if (paired) {
       // thread (16-row chunk, float4 column): every segment that STARTS in its chunk (running
       // past the chunk's end as needed) and, for chunk 0, the head segment begun in the
-      // previous tile -- the forward's EpLayerSeg walk
+      // previous tile -- the forward's EpLayerSeg walk; inside segments are turned into
+      // dh = da - C in place (measured against a one-pass form where every row re-sums its
+      // segment: 1.2 us faster per launch, profiles/r04_b_*)
+      constexpr int NCH = BM / 16;
       for (int q = tid; q < NCH * C4; q += NT) {
         const int ch = q / C4, c4 = q - ch * C4;
-        const int col = n0 + 4 * c4;
-        if (col >= N) continue;
+        const int cq = n0 + 4 * c4;
+        if (cq >= N) continue;
         int s = 16 * ch;
         const int end = min(16 * ch + 16, nrow);
         if (ch > 0)
@@ -98,7 +112,7 @@ struct EpLayerBwdSeg {
           if (head || tail) {
             const int b = dst_ptr[v], e = dst_ptr[v + 1];
             if (seg_tiles(b, e, BM) <= 2) {
-              float* g = dag + (int64_t)v * a.Hp + col;
+              float* g = dag + (int64_t)v * a.Hp + cq;
               atomicAdd(g, da.x);
               atomicAdd(g + 1, da.y);
               atomicAdd(g + 2, da.z);
@@ -120,28 +134,26 @@ struct EpLayerBwdSeg {
     }
     CGR_STAMP(4);
     // rows of crossing segments (or every row, unpaired): raw dm[rev(r)]; all others: dh -> the
-    // activation backward
-    const int vh = sd[0] == sd[1] ? sd[0] : -3;               // head segment's node, if any
-    const int vt = sd[nrow] == sd[nrow + 1] ? sd[nrow] : -3;  // tail segment's node, if any
-    const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
-    float dsig = 0.f;
+    // activation backward, one loop per activation (the switch outside the loop: no branch tree
+    // and no other activation's code inside it)
+    auto rows = [&](auto Ac) {
+      constexpr int A = decltype(Ac)::value;
 #pragma unroll
-    for (int it = 0; it < EIT; ++it) {
-      const int q = tid + it * NT;
-      if (q < BM * C4) {
-        const int r = q / C4, c4 = q - r * C4;
-        const int col = n0 + 4 * c4;
-        if (r < nrow && col < N) {
-          const float4 x = *reinterpret_cast<const float4*>(&C[r * LDC + 4 * c4]);
-          const int v = sd[r + 1];
-          const int64_t i = m0 + r;
-          if (!paired || v == vh || v == vt)
-            sc1_store4(raw + i * a.Hp + col, x);
-          else
-            bwd_row_apply<EDGE_INIT>(a, i, col, x, key, dsig, pv[it]);
-        }
+      for (int it = 0; it < EIT; ++it) {
+        const int r = er0 + RPP * it;
+        if (!eact || r >= nrow || col >= N) continue;
+        const float4 x = *reinterpret_cast<const float4*>(&C[r * LDC + 4 * ec4]);
+        const int v = sd[r + 1];
+        const int64_t i = m0 + r;
+        if (!paired || v == vh || v == vt)
+          sc1_store4(raw + i * a.Hp + col, x);
+        else
+          bwd_row_apply<EDGE_INIT, A>(a, i, col, x, key, dsig, pv[it]);
       }
-    }
+    };
+    if (a.act == ACT_RELU) rows(std::integral_constant<int, ACT_RELU>{});
+    else if (a.act == ACT_SILU) rows(std::integral_constant<int, ACT_SILU>{});
+    else rows(std::integral_constant<int, ACT_GELU>{});
 
     CGR_STAMP(5);
     // ---- hand-off: the last contributor of a crossing segment (or of the grid) completes it ----

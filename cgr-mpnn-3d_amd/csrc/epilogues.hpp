@@ -31,19 +31,24 @@ struct EpStore {
       if (c + 3 < N) o[3] = v.w;
     }
   }
-  // prefetched epilogue operands (gemm_nt_kernel issues every pre4 load of a tile before the
-  // accumulators go through LDS, so the loads overlap instead of one round trip per float4)
-  struct Ctx {};
-  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
-  typedef float4 Pre;
-  __device__ __forceinline__ Pre pre4(int r, int c) const {
-    if (!bias) return f4zero();
-    return make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
-                       bias[min(c + 3, N - 1)]);
+  // Epilogue protocol of the GEMM kernels: ctx(c) = the constants of the float4 column group at
+  // c (loaded once per thread: the split-bf16 NT keeps one column group per thread), pre4(r, c) =
+  // the row operands of one float4 piece (issued for a whole tile before the accumulators go
+  // through LDS), apply4p = the arithmetic and the stores.
+  struct Ctx {
+    float4 b;
+  };
+  __device__ __forceinline__ Ctx ctx(int c) const {
+    if (!bias) return Ctx{f4zero()};
+    return Ctx{make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
+                           bias[min(c + 3, N - 1)])};
   }
-  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& b, const Ctx&) const {
+  __device__ __forceinline__ void finish_ctx(Ctx&) const {}
+  struct Pre {};
+  __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&, const Ctx& cx) const {
     if (r >= M || c >= N) return;
-    v = f4add(v, b);
+    v = f4add(v, cx.b);
     float* o = C + (int64_t)r * ld + c;
     if (c + 4 <= N && ((ld & 3) == 0)) {
       *reinterpret_cast<float4*>(o) = v;
@@ -66,7 +71,8 @@ struct EpStoreRowScale {
   const float* dy;
   const int* node_graph;
   struct Ctx {};
-  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
+  __device__ __forceinline__ void finish_ctx(Ctx&) const {}
   typedef float Pre;
   __device__ __forceinline__ Pre pre4(int r, int) const { return dy[node_graph[min(r, M - 1)]]; }
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, Pre s, const Ctx&) const {
@@ -95,47 +101,85 @@ struct EpLayer {
   // internal [M, ld] buffers, ld % 4 == 0: whole float4 in bounds of the padded row; columns >= N
   // hold don't-care values (never read as data)
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
-    apply4p(r, c, v, pre4(r, c), ctx());
+    Ctx cx = ctx(c);
+    finish_ctx(cx);
+    apply4p<-1>(r, c, v, pre4(r, c), cx);
   }
-  // prefetch: h0 and bias of a float4 piece, unconditional loads from clamped in-bounds addresses
-  // (no branch around the loads); the scalars (sigma, dropout key) once per workgroup
+  // per column group: bias and the scalars (sigma, dropout key); per piece: h0, an unconditional
+  // load from a clamped in-bounds address (no branch around the loads)
   struct Ctx {
     float sg;
     uint64_t key;
+    float4 b;
   };
-  __device__ __forceinline__ Ctx ctx() const {
-    return Ctx{sigma ? sigma[0] : 1.f, thresh ? *seed : 0ull};
-  }
-  struct Pre {
-    float4 h0, b;
-  };
-  __device__ __forceinline__ Pre pre4(int r, int c) const {
-    const bool ok = r < M && c < N;
-    return Pre{*reinterpret_cast<const float4*>(h0 + (ok ? (int64_t)r * ld + c : 0)),
+  // ctx(c): the per-column vector loads (issued early); finish_ctx: the workgroup scalars (scalar
+  // loads count against lgkmcnt, which every LDS barrier drains: loaded at the epilogue)
+  __device__ __forceinline__ Ctx ctx(int c) const {
+    return Ctx{1.f, 0ull,
                make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
                            bias[min(c + 3, N - 1)])};
   }
+  __device__ __forceinline__ void finish_ctx(Ctx& cx) const {
+    cx.sg = sigma ? sigma[0] : 1.f;
+    cx.key = thresh ? *seed : 0ull;
+  }
+  struct Pre {
+    float4 h0;
+  };
+  __device__ __forceinline__ Pre pre4(int r, int c) const {
+    const bool ok = r < M && c < N;
+    return Pre{*reinterpret_cast<const float4*>(h0 + (ok ? (int64_t)r * ld + c : 0))};
+  }
+  // A >= 0: the activation as a compile-time constant (the GEMM kernel switches on `act` once,
+  // outside its epilogue loop: kAct); A < 0: `act` at run time
+  static constexpr bool kAct = true;
+  template <int A = -1>
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& p,
                                           const Ctx& cx) const {
     if (r >= M || c >= N) return;
-    const int64_t o = (int64_t)r * ld + c;
     float z[4] = {v.x, v.y, v.z, v.w};
     const float h0v[4] = {p.h0.x, p.h0.y, p.h0.z, p.h0.w};
-    const float bv[4] = {p.b.x, p.b.y, p.b.z, p.b.w};
+    const float bv[4] = {cx.b.x, cx.b.y, cx.b.z, cx.b.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) z[k] = (z[k] + bv[k]) + cx.sg * h0v[k];
-    if (pre) *reinterpret_cast<float4*>(pre + o) = make_float4(z[0], z[1], z[2], z[3]);
+    finish4<A>(r, c, make_float4(z[0], z[1], z[2], z[3]), cx);
+  }
+  // pre = z -> act -> dropout -> h stored (and returned); the caller checked r < M, c < N
+  template <int A = -1>
+  __device__ __forceinline__ float4 finish4(int r, int c, float4 z4, const Ctx& cx) const {
+    const int64_t o = (int64_t)r * ld + c;
+    const float z[4] = {z4.x, z4.y, z4.z, z4.w};
+    if (pre) *reinterpret_cast<float4*>(pre + o) = z4;
     float h[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      h[k] = act_fwd(z[k], act);
+      h[k] = act_fwd(z[k], A < 0 ? act : A);
       if (thresh)
         h[k] = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
                                                                                     : 0.f;
       else
         h[k] *= scale;
     }
-    *reinterpret_cast<float4*>(hout + o) = make_float4(h[0], h[1], h[2], h[3]);
+    const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<float4*>(hout + o) = hv;
+    return hv;
+  }
+  // the addend (b + sigma h0) taken into the accumulators in the GEMM's MFMA layout
+  // (gemm_b3nt_kernel kAddend): loads of element (r, c) from clamped in-bounds addresses, then
+  // z = (acc + b) + sigma h0 -- the operation order of apply4p, so both forms agree bit for bit
+  static constexpr bool kAddend = true;
+  __device__ __forceinline__ Ctx ctx_add() const { return Ctx{1.f, 0ull, f4zero()}; }
+  __device__ __forceinline__ float add_row(int r, int c) const {
+    return h0[(int64_t)(r < M ? r : M - 1) * ld + (c < N ? c : N - 1)];
+  }
+  __device__ __forceinline__ float add_col(int c) const { return bias[c < N ? c : N - 1]; }
+  __device__ __forceinline__ float add_apply(float acc, float h0v, float b, const Ctx& cx) const {
+    return (acc + b) + cx.sg * h0v;
+  }
+  template <int A = -1>
+  __device__ __forceinline__ void apply4z(int r, int c, float4 z, const Ctx& cx) const {
+    if (r >= M || c >= N) return;
+    finish4<A>(r, c, z, cx);
   }
 };
 
@@ -154,30 +198,22 @@ struct EpLayerSeg : EpLayer {
   float* part;         // [tiles, 2, BN] their partial sums (slot_of)
   int* cnt;            // [nodes * tiles_n] tickets (zero on entry, left zero)
   int tiles_n;
-  // apply4p that also returns the stored h (rows / columns outside: v unchanged)
+  // apply4p / apply4z that also return the stored h (rows / columns outside: v unchanged)
+  template <int A = -1>
   __device__ __forceinline__ float4 apply4p_h(int r, int c, float4 v, const Pre& p,
                                               const Ctx& cx) const {
     if (r >= M || c >= N) return v;
-    const int64_t o = (int64_t)r * ld + c;
     float z[4] = {v.x, v.y, v.z, v.w};
     const float h0v[4] = {p.h0.x, p.h0.y, p.h0.z, p.h0.w};
-    const float bv[4] = {p.b.x, p.b.y, p.b.z, p.b.w};
+    const float bv[4] = {cx.b.x, cx.b.y, cx.b.z, cx.b.w};
 #pragma unroll
     for (int k = 0; k < 4; ++k) z[k] = (z[k] + bv[k]) + cx.sg * h0v[k];
-    if (pre) *reinterpret_cast<float4*>(pre + o) = make_float4(z[0], z[1], z[2], z[3]);
-    float h[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      h[k] = act_fwd(z[k], act);
-      if (thresh)
-        h[k] = drop_keep(cx.key, (uint32_t)layer, (uint64_t)r * N + c + k, thresh) ? h[k] * scale
-                                                                                    : 0.f;
-      else
-        h[k] *= scale;
-    }
-    const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
-    *reinterpret_cast<float4*>(hout + o) = hv;
-    return hv;
+    return this->template finish4<A>(r, c, make_float4(z[0], z[1], z[2], z[3]), cx);
+  }
+  template <int A = -1>
+  __device__ __forceinline__ float4 apply4z_h(int r, int c, float4 z, const Ctx& cx) const {
+    if (r >= M || c >= N) return z;
+    return this->template finish4<A>(r, c, z, cx);
   }
 };
 
@@ -206,7 +242,8 @@ struct EpSplit2 {
     }
   }
   struct Ctx {};
-  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
+  __device__ __forceinline__ void finish_ctx(Ctx&) const {}
   struct Pre {};
   __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&, const Ctx&) const {
@@ -224,29 +261,51 @@ struct EpReadoutQ {
   int64_t ld;
   int M, N;
   int act;
-  struct Ctx {};
-  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  struct Ctx {
+    float4 b;
+  };
+  __device__ __forceinline__ Ctx ctx(int c) const {
+    return Ctx{make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
+                           bias[min(c + 3, N - 1)])};
+  }
+  __device__ __forceinline__ void finish_ctx(Ctx&) const {}
   struct Pre {
-    float4 q, b;
+    float4 q;
   };
   __device__ __forceinline__ Pre pre4(int r, int c) const {
     const bool ok = r < M && c < N;
-    return Pre{*reinterpret_cast<const float4*>(Q + (ok ? (int64_t)r * ld + c : 0)),
-               make_float4(bias[min(c, N - 1)], bias[min(c + 1, N - 1)], bias[min(c + 2, N - 1)],
-                           bias[min(c + 3, N - 1)])};
+    return Pre{*reinterpret_cast<const float4*>(Q + (ok ? (int64_t)r * ld + c : 0))};
   }
+  static constexpr bool kAct = true;  // see EpLayer
+  template <int A = -1>
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre& p,
-                                          const Ctx&) const {
+                                          const Ctx& cx) const {
+    if (r >= M || c >= N) return;
+    apply4z<A>(r, c, f4add(f4add(v, p.q), cx.b), cx);
+  }
+  // the addend (Q + b) taken into the accumulators in MFMA layout (gemm_b3nt_kernel kAddend),
+  // z = (acc + Q) + b in apply4p's order
+  static constexpr bool kAddend = true;
+  __device__ __forceinline__ Ctx ctx_add() const { return Ctx{f4zero()}; }
+  __device__ __forceinline__ float add_row(int r, int c) const {
+    return Q[(int64_t)(r < M ? r : M - 1) * ld + (c < N ? c : N - 1)];
+  }
+  __device__ __forceinline__ float add_col(int c) const { return bias[c < N ? c : N - 1]; }
+  __device__ __forceinline__ float add_apply(float acc, float q, float b, const Ctx&) const {
+    return (acc + q) + b;
+  }
+  template <int A = -1>
+  __device__ __forceinline__ void apply4z(int r, int c, float4 z4, const Ctx&) const {
     if (r >= M || c >= N) return;
     const int64_t o = (int64_t)r * ld + c;
-    const float4 z4 = f4add(f4add(v, p.q), p.b);
     const float z[4] = {z4.x, z4.y, z4.z, z4.w};
+    const int ac = A < 0 ? act : A;
     if (zn) *reinterpret_cast<float4*>(zn + o) = make_float4(z[0], z[1], z[2], z[3]);
     *reinterpret_cast<float4*>(hn + o) =
-        make_float4(act_fwd(z[0], act), act_fwd(z[1], act), act_fwd(z[2], act), act_fwd(z[3], act));
+        make_float4(act_fwd(z[0], ac), act_fwd(z[1], ac), act_fwd(z[2], ac), act_fwd(z[3], ac));
   }
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
-    apply4p(r, c, v, pre4(r, c), ctx());
+    apply4p<-1>(r, c, v, pre4(r, c), ctx(c));
   }
 };
 
@@ -270,7 +329,8 @@ struct EpReadout {
         make_float4(act_fwd(z[0], act), act_fwd(z[1], act), act_fwd(z[2], act), act_fwd(z[3], act));
   }
   struct Ctx {};
-  __device__ __forceinline__ Ctx ctx() const { return Ctx{}; }
+  __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
+  __device__ __forceinline__ void finish_ctx(Ctx&) const {}
   struct Pre {};
   __device__ __forceinline__ Pre pre4(int, int) const { return Pre{}; }
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, const Pre&, const Ctx&) const {

@@ -135,7 +135,8 @@ struct LdGatherRows {
 // A(v, k) = act'(m[v, k]) with m = hn (ReLU: hn > 0) or zn (internal [M, ld] buffers, ld % 4 == 0).
 // dzn = dy[graph(v)] wf[k] act'(zn[v, k]) factors into this, a per-k scale folded into the weight
 // image (B3PackJob::kscale) and a per-row scale applied by the epilogue (EpStoreRowScale).
-struct LdActGrad {
+template <int ACT = -1>  // ACT >= 0: the activation as a compile-time constant (main-loop code)
+struct LdActGradT {
   const float* m;
   int64_t ld;
   int act;
@@ -143,6 +144,7 @@ struct LdActGrad {
     const float* p;
     bool ok;
   };
+using LdActGrad = LdActGradT<-1>;
   typedef float4 Raw;
   __device__ __forceinline__ Row row(int r, int limit) const {
     const bool ok = r < limit;
@@ -152,8 +154,9 @@ struct LdActGrad {
     return *reinterpret_cast<const float4*>(rw.p + (k < K ? k : 0));
   }
   __device__ __forceinline__ float4 combine_nm(const Raw& v) const {
-    return make_float4(act_grad(v.x, act), act_grad(v.y, act), act_grad(v.z, act),
-                       act_grad(v.w, act));
+    const int ac = ACT < 0 ? act : ACT;
+    return make_float4(act_grad(v.x, ac), act_grad(v.y, ac), act_grad(v.z, ac),
+                       act_grad(v.w, ac));
   }
   __device__ __forceinline__ float4 combine(const Raw& v, const Row& rw, int k, int K) const {
     return mask4(combine_nm(v), rw.ok, k, K);
@@ -470,7 +473,6 @@ gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int K, int tiles_n) {
   // tile instead of one per float4 piece.
   constexpr int C4 = BN / 4;
   constexpr int EIT = (BM * C4 + NT - 1) / NT;
-  const typename EP::Ctx cx = ep.ctx();
   typename EP::Pre pv[EIT];
 #pragma unroll
   for (int it = 0; it < EIT; ++it) {
@@ -493,6 +495,8 @@ gemm_nt_kernel(AL al, BL bl, EP ep, int M, int N, int K, int tiles_n) {
     if (q < BM * C4) {
       const int r = q / C4, c4 = q - r * C4;
       const float4 v = *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]);
+      typename EP::Ctx cx = ep.ctx(n0 + 4 * c4);
+      ep.finish_ctx(cx);
       ep.apply4p(m0 + r, n0 + 4 * c4, v, pv[it], cx);
     }
   }

@@ -177,6 +177,25 @@ struct b3_ep_tile : std::false_type {};
 template <class EP>
 struct b3_ep_tile<EP, std::void_t<decltype(EP::kTile)>> : std::bool_constant<EP::kTile> {};
 
+// epilogue functors with kAddend = true take their addend (bias, skip term, Q, ...) into the
+// accumulators in MFMA layout: its loads are issued in the last k step (EpLayer, EpReadoutQ)
+template <class EP, class = void>
+struct b3_ep_addend : std::false_type {};
+template <class EP>
+struct b3_ep_addend<EP, std::void_t<decltype(EP::kAddend)>> : std::bool_constant<EP::kAddend> {};
+#ifdef CGR_NO_ADDEND
+template <class EP>
+struct b3_ep_addend_off : std::false_type {};
+#define b3_ep_addend b3_ep_addend_off
+#endif
+
+// epilogue functors with kAct = true apply an activation `act`: the kernel switches on it once,
+// outside its epilogue loop, and hands it to the functor as a template constant
+template <class EP, class = void>
+struct b3_ep_act : std::false_type {};
+template <class EP>
+struct b3_ep_act<EP, std::void_t<decltype(EP::kAct)>> : std::bool_constant<EP::kAct> {};
+
 template <int WAVES, int RF, int NF>
 struct B3NtShape {
   static constexpr int NT = WAVES * 64;
@@ -218,6 +237,34 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + B3_BK - 1) / B3_BK;
   const int sw = fg ^ lds_swz(fr);  // lds_swz(16 j + fr) == lds_swz(fr)
+
+  // ---- epilogue mapping: one float4 column group per thread, rows er0 + RPP * it ----
+  constexpr int C4 = BN / 4;
+  constexpr int RPP = NT / C4;                // rows per pass
+  constexpr int EIT = (BM + RPP - 1) / RPP;   // passes
+  constexpr bool SEG = EP::kSeg;  // the epilogue also sums the tile's dst segments (EpLayerSeg)
+  // the whole tile goes to the functor (EpLayerBwdSeg: ep_bwd.hpp)
+  constexpr bool TILE = b3_ep_tile<EP>::value;
+  static_assert(NT >= BM + 2 && RPP >= 1, "one dst per thread; one row group per pass");
+  const bool eact = tid < RPP * C4;
+  const int ec4 = eact ? tid % C4 : 0, er0 = tid / C4;
+  const int ecol = n0 + 4 * ec4;
+  // issued in the prologue behind the first operand loads, used after the main loop: the column
+  // group's constants (bias, ...) and, for the segmented epilogues, the dst of rows
+  // m0 - 1 .. m0 + BM (one per thread)
+  typename EP::Ctx cx;
+  int sdv = 0;
+  auto epilogue_consts = [&]() {
+    if constexpr (b3_ep_addend<EP>::value)
+      cx = ep.ctx_add();  // the column constants travel with the addend
+    else
+      cx = ep.ctx(ecol);
+    if constexpr (SEG || TILE) {
+      const int r = m0 - 1 + tid;
+      const int d = ep.dst_s[min(max(r, 0), M - 1)];
+      sdv = (r >= 0 && r < M) ? d : -1 - (r >= M);  // distinct sentinels outside [0, M)
+    }
+  };
 
   // ---- A: RF row fragments per lane, two float4 fetches per fragment per k step ----
   typename AL::Row arow[RF];
@@ -377,6 +424,92 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     __syncthreads();
   };
 
+  // The last step (tail): no operand loads, B stores or A split are left to issue (the main
+  // steps fetch two steps ahead); for an addend epilogue it issues the addend loads in the load
+  // slots instead: the addend of fragment column j is loaded beside the MFMAs of pair j / 2, so
+  // its HBM traffic overlaps the matrix work instead of following it.  (A two-step tail that
+  // also splits A of the last step spilled 16-22 VGPRs on the gathered-A kernels.)
+  constexpr bool ADD = b3_ep_addend<EP>::value;
+  float arow_v[ADD ? RF : 1][ADD ? NF : 1][4];
+  float acol_v[ADD ? NF : 1];
+  // the lane coordinates of the addend loads are recomputed behind an opaque copy of the thread
+  // id: shared with the prologue's, they would stay live across the main loop (spills)
+  int otid = 0;
+  auto add_loads = [&](int j) {
+    if constexpr (ADD) {
+      const int ofr = otid & 15, ofg = (otid & 63) >> 4, ow = otid >> 6;
+      const int col = n0 + j * 16 + ofr;
+#pragma unroll
+      for (int i = 0; i < RF; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          arow_v[i][j][r] = ep.add_row(m0 + (ow * RF + i) * 16 + ofg * 4 + r, col);
+    }
+  };
+  auto tstep = [&](int cb, const b3_u4 (&afc)[RF][3], const ARaw* xa, b3_u4 (&afn)[RF][3],
+                   int ksn, bool prefetch, bool last) {
+    const b3_u4* Bs = b3_lds + cb * BU4;
+    constexpr int LDA = B3_LDA < NF ? B3_LDA : NF - 1;
+    constexpr int RING = LDA + 2;
+    b3_u4 bq[RING][3];
+    auto rd = [&](int j) {
+      const int o = (j * 16 + fr) * 4 + sw;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        bq[j % RING][q] = Bs[q * BN * 4 + o];
+    };
+#pragma unroll
+    for (int j = 0; j < LDA; ++j) rd(j);
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int j = 2 * p;
+      const bool two = j + 1 < NF;
+      int nrd = 0;
+      if (j + LDA < NF) {
+        rd(j + LDA);
+        nrd += 3;
+      }
+      if (two && j + 1 + LDA < NF) {
+        rd(j + 1 + LDA);
+        nrd += 3;
+      }
+      const b3_u4(&b)[3] = bq[j % RING];
+      const b3_u4(&c)[3] = bq[(j + 1) % RING];
+#pragma unroll
+      for (int i = 0; i < RF; ++i) {
+        floatx4 x = acc[i][j], y = two ? acc[i][j + 1] : x;
+        x = b3_mfma(afc[i][1], b[1], x);
+        if (two) y = b3_mfma(afc[i][1], c[1], y);
+        x = b3_mfma(afc[i][0], b[2], x);
+        if (two) y = b3_mfma(afc[i][0], c[2], y);
+        x = b3_mfma(afc[i][2], b[0], x);
+        if (two) y = b3_mfma(afc[i][2], c[0], y);
+        x = b3_mfma(afc[i][0], b[1], x);
+        if (two) y = b3_mfma(afc[i][0], c[1], y);
+        x = b3_mfma(afc[i][1], b[0], x);
+        if (two) y = b3_mfma(afc[i][1], c[0], y);
+        x = b3_mfma(afc[i][0], b[0], x);
+        if (two) y = b3_mfma(afc[i][0], c[0], y);
+        acc[i][j] = x;
+        if (two) acc[i][j + 1] = y;
+      }
+      int nvm = 0;
+      if (ADD && prefetch) {
+        add_loads(j);
+        if (two) add_loads(j + 1);
+        nvm = (two ? 2 : 1) * 4 * RF;
+      }
+      if (xa && p == NP / 2) splitA(*xa, afn, ksn);
+      constexpr int MQ = 4 * RF;
+      b3_sgb<0x100>(nrd);
+      if (two) b3_sgb<0x008>(MQ); else b3_sgb<0x008>(MQ / 2);
+      b3_sgb<0x020>(nvm);
+      if (two) b3_sgb<0x008>(2 * MQ); else b3_sgb<0x008>(MQ + MQ / 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (last) __syncthreads();
+  };
+
   {  // prologue: buffers 0, 1 <- B(0), B(1); afr0 <- A(0); raw set 0 <- A(1), B(2)
     ARaw a0, xa0, xa1;
     BRaw b0, b1, xb0, xb1;
@@ -391,41 +524,53 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     splitA(a0, afr0, 0);
     __syncthreads();
     CGR_STAMP(1);
+    epilogue_consts();  // after the prologue barrier: not waited for by it
     int cb = 0;  // LDS buffer of step ks (ks % 3)
-    for (int ks = 0; ks < nk; ks += 2) {
+    const int nmain = nk - 1;  // steps before the tail (the last step)
+    for (int ks = 0; ks < nmain; ks += 2) {
       // even step: consume set 0 (A(ks+1), B(ks+2)), fill set 1 with A(ks+2), B(ks+3)
       step(cb, afr0, xb0, cb == 0 ? 2 : cb - 1, xa0, afr1, ks + 1, xa1, ks + 2, xb1, ks + 3);
-      if (ks + 1 >= nk) break;
       cb = cb == 2 ? 0 : cb + 1;
+      if (ks + 1 >= nmain) break;
       // odd step: consume set 1 (A(ks+2), B(ks+3)), fill set 0 with A(ks+3), B(ks+4)
       step(cb, afr1, xb1, cb == 0 ? 2 : cb - 1, xa1, afr0, ks + 2, xa0, ks + 3, xb0, ks + 4);
       cb = cb == 2 ? 0 : cb + 1;
     }
+    // tail: the last step uses fragment set nmain % 2 (split by the step before), moved into set
+    // 0 so that the tail is one piece of code
+    if (nmain & 1) {
+#pragma unroll
+      for (int i = 0; i < RF; ++i)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) afr0[i][q] = afr1[i][q];
+    }
+    if constexpr (ADD) asm volatile("v_mov_b32 %0, %1" : "=v"(otid) : "v"(tid));
+    tstep(cb, afr0, nullptr, afr1, 0, true, true);
   }
 
   CGR_STAMP(2);
   // ---- epilogue (the stage buffers are dead after the last barrier) ----
-  constexpr int C4 = BN / 4;
-  constexpr int EIT = (BM * C4 + NT - 1) / NT;
-  const typename EP::Ctx cx = ep.ctx();
-  typename EP::Pre pv[EIT];
+  ep.finish_ctx(cx);
+  if constexpr (ADD) {  // the addend into the accumulators (the operation order of the apply)
 #pragma unroll
-  for (int it = 0; it < EIT; ++it) {
-    const int q = min(tid + it * NT, BM * C4 - 1);
-    const int r = q / C4, c4 = q - r * C4;
-    pv[it] = ep.pre4(m0 + r, n0 + 4 * c4);
+    for (int j = 0; j < NF; ++j) acol_v[j] = ep.add_col(n0 + j * 16 + fr);  // L2-resident
+#pragma unroll
+    for (int i = 0; i < RF; ++i)
+#pragma unroll
+      for (int j = 0; j < NF; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          acc[i][j][r] = ep.add_apply(acc[i][j][r], arow_v[i][j][r], acol_v[j], cx);
+  }
+  typename EP::Pre pv[EIT];
+  if constexpr (!ADD) {
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) pv[it] = ep.pre4(m0 + min(er0 + RPP * it, BM - 1), ecol);
   }
   float* C = reinterpret_cast<float*>(b3_lds);
-  constexpr bool SEG = EP::kSeg;  // the epilogue also sums the tile's dst segments (EpLayerSeg)
-  // the whole tile goes to the functor (EpLayerBwdSeg: ep_bwd.hpp)
-  constexpr bool TILE = b3_ep_tile<EP>::value;
   int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG / TILE: dst of rows m0 - 1 .. m0 + BM
-  if constexpr (SEG || TILE) {
-    for (int q = tid; q < BM + 2; q += NT) {
-      const int r = m0 - 1 + q;
-      sd[q] = (r >= 0 && r < M) ? ep.dst_s[r] : -1 - (r >= M);  // distinct sentinels
-    }
-  }
+  if constexpr (SEG || TILE)
+    if (tid < BM + 2) sd[tid] = sdv;
 #pragma unroll
   for (int i = 0; i < RF; ++i)
 #pragma unroll
@@ -436,19 +581,34 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   __syncthreads();
   CGR_STAMP(3);
   if constexpr (TILE) {
-    ep.template tile<BM, BN, NT, S::LDC, EIT>(pv, C, sd, m0, n0, tile, tid);
+    ep.template tile<BM, BN, NT, S::LDC, EIT, RPP>(pv, C, sd, m0, n0, tile, tid);
   } else {
+  auto apply_pass = [&](auto Ac) {
+    constexpr int A = decltype(Ac)::value;
 #pragma unroll
-  for (int it = 0; it < EIT; ++it) {
-    const int q = tid + it * NT;
-    if (q < BM * C4) {
-      const int r = q / C4, c4 = q - r * C4;
-      float4* cp = reinterpret_cast<float4*>(&C[r * S::LDC + 4 * c4]);
-      if constexpr (SEG)
-        *cp = ep.apply4p_h(m0 + r, n0 + 4 * c4, *cp, pv[it], cx);  // keep h for the sums
-      else
-        ep.apply4p(m0 + r, n0 + 4 * c4, *cp, pv[it], cx);
+    for (int it = 0; it < EIT; ++it) {
+      const int r = er0 + RPP * it;
+      if (eact && r < BM) {
+        float4* cp = reinterpret_cast<float4*>(&C[r * S::LDC + 4 * ec4]);
+        if constexpr (SEG && ADD)
+          *cp = ep.template apply4z_h<A>(m0 + r, ecol, *cp, cx);  // keep h for the sums
+        else if constexpr (SEG)
+          *cp = ep.template apply4p_h<A>(m0 + r, ecol, *cp, pv[it], cx);
+        else if constexpr (ADD)
+          ep.template apply4z<A>(m0 + r, ecol, *cp, cx);
+        else if constexpr (b3_ep_act<EP>::value)
+          ep.template apply4p<A>(m0 + r, ecol, *cp, pv[it], cx);
+        else
+          ep.apply4p(m0 + r, ecol, *cp, pv[it], cx);
+      }
     }
+  };
+  if constexpr (b3_ep_act<EP>::value) {  // one loop per activation, chosen once
+    if (ep.act == ACT_RELU) apply_pass(std::integral_constant<int, ACT_RELU>{});
+    else if (ep.act == ACT_SILU) apply_pass(std::integral_constant<int, ACT_SILU>{});
+    else apply_pass(std::integral_constant<int, ACT_GELU>{});
+  } else {
+    apply_pass(std::integral_constant<int, -1>{});
   }
   CGR_STAMP(4);
   if constexpr (SEG) {
@@ -460,6 +620,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     // zero: p + q == q + p, deterministic); one over three or more row tiles (a hub node,
     // in-degree > BM + 1) leaves its partial in a slot fixed by the data and its last
     // contributor sums the slots in row-tile order -- deterministic for every in-degree.
+    // (Measured against one thread per segment head over the apply pass's row mapping: the
+    // chunk walk is 0.9 us faster per launch, profiles/r04_b_*.)
     __syncthreads();
     const int nrow = min(BM, M - m0);
     constexpr int NCH = BM / 16;

@@ -281,9 +281,16 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // the epilogue, the column factor in the weight image (gnn_fwd.hip), act' in the A loader
   {
     ProfScope _p("gemm_nt_readout_bwd", st);
-    HIP_RET(launch_b3nt(LdActGrad{d.act == ACT_RELU ? fv.hn : fv.zn, Hp, d.act},
-                        static_cast<const b3_u4*>(fv.b3rob),
-                        EpStoreRowScale{ds, Hp, N, H, dy, iv.node_graph}, N, H, H, st));
+    const float* m = d.act == ACT_RELU ? fv.hn : fv.zn;
+    const b3_u4* img = static_cast<const b3_u4*>(fv.b3rob);
+    const EpStoreRowScale ep{ds, Hp, N, H, dy, iv.node_graph};
+    // the activation derivative in the A loader, specialised per activation (main-loop code)
+    if (d.act == ACT_RELU)
+      HIP_RET(launch_b3nt(LdActGradT<ACT_RELU>{m, Hp, d.act}, img, ep, N, H, H, st));
+    else if (d.act == ACT_SILU)
+      HIP_RET(launch_b3nt(LdActGradT<ACT_SILU>{m, Hp, d.act}, img, ep, N, H, H, st));
+    else
+      HIP_RET(launch_b3nt(LdActGradT<ACT_GELU>{m, Hp, d.act}, img, ep, N, H, H, st));
   }
 
   // learnable-skip partial-sum slots per layer (bwd_dsig_slots)

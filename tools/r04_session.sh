@@ -48,3 +48,7 @@ if [ "${PROBE:-0}" = "1" ]; then
   AMD_LOG_LEVEL=${PROBE_LOG:-1} timeout -k 10 240 python -u tools/rccl_teardown_probe.py > "$OUT/probe.log" 2>&1; rc=$?
   echo "probe rc=$rc"; grep -v "^Extension modules" "$OUT/probe.log" | tail -40
 fi
+if [ -n "${AB_VARIANTS:-}" ]; then
+  st "class A/B: $AB_VARIANTS"
+  TAG=${TAG:-r04_s}-ab VARIANTS="$AB_VARIANTS" ROUNDS=${AB_ROUNDS:-2} bash tools/ab_classes.sh || exit 1
+fi
