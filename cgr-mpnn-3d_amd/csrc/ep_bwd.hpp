@@ -87,55 +87,16 @@ struct EpLayerBwdSeg {
     const int vt = sd[nrow] == sd[nrow + 1] ? sd[nrow] : -3;  // tail segment's node, if any
     const uint64_t key = (!EDGE_INIT && a.thresh) ? *a.seed : 0;
     float dsig = 0.f;
-    if (paired) {
-      // thread (16-row chunk, float4 column): every segment that STARTS in its chunk (running
-      // past the chunk's end as needed) and, for chunk 0, the head segment begun in the
-      // previous tile -- the forward's EpLayerSeg walk; inside segments are turned into
-      // dh = da - C in place (measured against a one-pass form where every row re-sums its
-      // segment: 1.2 us faster per launch, profiles/r04_b_*)
-      constexpr int NCH = BM / 16;
-      for (int q = tid; q < NCH * C4; q += NT) {
-        const int ch = q / C4, c4 = q - ch * C4;
-        const int cq = n0 + 4 * c4;
-        if (cq >= N) continue;
-        int s = 16 * ch;
-        const int end = min(16 * ch + 16, nrow);
-        if (ch > 0)
-          while (s < end && sd[s + 1] == sd[s]) ++s;
-        while (s < end) {
-          const int v = sd[s + 1];
-          float4 da = f4zero();
-          int r = s;
-          for (; r < nrow && sd[r + 1] == v; ++r)
-            da = f4add(da, *reinterpret_cast<const float4*>(&C[r * LDC + 4 * c4]));
-          const bool head = s == 0 && sd[0] == v, tail = r == nrow && sd[nrow + 1] == v;
-          if (head || tail) {
-            const int b = dst_ptr[v], e = dst_ptr[v + 1];
-            if (seg_tiles(b, e, BM) <= 2) {
-              float* g = dag + (int64_t)v * a.Hp + cq;
-              atomicAdd(g, da.x);
-              atomicAdd(g + 1, da.y);
-              atomicAdd(g + 2, da.z);
-              atomicAdd(g + 3, da.w);
-            } else {
-              const int slot = slot_of(m0 / BM, b / BM);
-              sc1_store4(part + ((int64_t)tile_id * 2 + slot) * BN + 4 * c4, da);
-            }
-          } else {
-            for (int k = s; k < r; ++k) {
-              float4* cp = reinterpret_cast<float4*>(&C[k * LDC + 4 * c4]);
-              *cp = f4sub(da, *cp);
-            }
-          }
-          s = r;
-        }
-      }
-      __syncthreads();
-    }
+    // one pass, every row independent: row r's dst segment [s, e) inside the tile from the
+    // tile's segment-start mask (rows are dst-sorted; with paired edges its rows are exactly the
+    // dm rows its node sums), da = the segment's sum in row order (the same for every row of the
+    // segment), dh = da - dm[rev(r)] -> the activation backward.  A segment crossing a row tile
+    // (or every row, unpaired) stores its raw rows for the completer, and its first row in the
+    // tile hands over the partial sum.  One loop per activation (the switch outside the loop).
+    const uint32_t* smask = reinterpret_cast<const uint32_t*>(sd + BM + 2 + 8);
+    const uint64_t mlo = smask[0] | ((uint64_t)smask[1] << 32);
+    const uint64_t mhi = smask[2] | ((uint64_t)smask[3] << 32);
     CGR_STAMP(4);
-    // rows of crossing segments (or every row, unpaired): raw dm[rev(r)]; all others: dh -> the
-    // activation backward, one loop per activation (the switch outside the loop: no branch tree
-    // and no other activation's code inside it)
     auto rows = [&](auto Ac) {
       constexpr int A = decltype(Ac)::value;
 #pragma unroll
@@ -143,12 +104,35 @@ struct EpLayerBwdSeg {
         const int r = er0 + RPP * it;
         if (!eact || r >= nrow || col >= N) continue;
         const float4 x = *reinterpret_cast<const float4*>(&C[r * LDC + 4 * ec4]);
-        const int v = sd[r + 1];
         const int64_t i = m0 + r;
-        if (!paired || v == vh || v == vt)
+        if (!paired) {
           sc1_store4(raw + i * a.Hp + col, x);
-        else
-          bwd_row_apply<EDGE_INIT, A>(a, i, col, x, key, dsig, pv[it]);
+          continue;
+        }
+        const int v = sd[r + 1];
+        const int s = seg_first(mlo, mhi, r), e = seg_end(mlo, mhi, r);
+        const bool head = s == 0 && sd[0] == v, tail = e == nrow && sd[nrow + 1] == v;
+        float4 da = f4zero();
+        for (int k = s; k < e; ++k)
+          da = f4add(da, *reinterpret_cast<const float4*>(&C[k * LDC + 4 * ec4]));
+        if (head || tail) {
+          sc1_store4(raw + i * a.Hp + col, x);
+          if (r == s) {
+            const int b = dst_ptr[v], ee = dst_ptr[v + 1];
+            if (seg_tiles(b, ee, BM) <= 2) {
+              float* g = dag + (int64_t)v * a.Hp + col;
+              atomicAdd(g, da.x);
+              atomicAdd(g + 1, da.y);
+              atomicAdd(g + 2, da.z);
+              atomicAdd(g + 3, da.w);
+            } else {
+              const int slot = slot_of(m0 / BM, b / BM);
+              sc1_store4(part + ((int64_t)tile_id * 2 + slot) * BN + 4 * ec4, da);
+            }
+          }
+        } else {
+          bwd_row_apply<EDGE_INIT, A>(a, i, col, f4sub(da, x), key, dsig, pv[it]);
+        }
       }
     };
     if (a.act == ACT_RELU) rows(std::integral_constant<int, ACT_RELU>{});

@@ -254,6 +254,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   // m0 - 1 .. m0 + BM (one per thread)
   typename EP::Ctx cx;
   int sdv = 0;
+  bool sstart = true;  // row tid starts a dst segment in the tile (handoff.hpp seg_*)
   auto epilogue_consts = [&]() {
     if constexpr (b3_ep_addend<EP>::value)
       cx = ep.ctx_add();  // the column constants travel with the addend
@@ -263,6 +264,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       const int r = m0 - 1 + tid;
       const int d = ep.dst_s[min(max(r, 0), M - 1)];
       sdv = (r >= 0 && r < M) ? d : -1 - (r >= M);  // distinct sentinels outside [0, M)
+      const int d1 = ep.dst_s[min(r + 1, M - 1)];    // row tid itself
+      sstart = tid == 0 || r + 1 >= M || d1 != d;
     }
   };
 
@@ -569,8 +572,20 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   }
   float* C = reinterpret_cast<float*>(b3_lds);
   int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG / TILE: dst of rows m0 - 1 .. m0 + BM
-  if constexpr (SEG || TILE)
+  // segment-start mask of the tile's rows: words 8..11 of the 16 scratch words after sd
+  uint32_t* smask = reinterpret_cast<uint32_t*>(sd + BM + 2 + 8);
+  if constexpr (SEG || TILE) {
+    static_assert(BM == 64 || BM == 128, "segment mask: one or two 64-row words");
     if (tid < BM + 2) sd[tid] = sdv;
+    if (tid < BM) {
+      const uint64_t b = __ballot(sstart);
+      if ((tid & 63) == 0) {
+        smask[2 * (tid >> 6)] = (uint32_t)b;
+        smask[2 * (tid >> 6) + 1] = (uint32_t)(b >> 32);
+      }
+    }
+    if (BM == 64 && tid == 0) smask[2] = smask[3] = 0xffffffffu;  // rows 64.. (none): starts
+  }
 #pragma unroll
   for (int i = 0; i < RF; ++i)
 #pragma unroll
@@ -612,51 +627,42 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   }
   CGR_STAMP(4);
   if constexpr (SEG) {
-    // a[v] = sum_{dst(i) = v} h[i] for the tile's columns (GNN.py:134): thread (16-row chunk,
-    // float4 column) sums, in row order, every segment that STARTS in its chunk (running past
-    // the chunk's end as needed), and the chunk-0 thread also the head segment begun in the
-    // previous tile.  A segment inside the tile is stored; one crossing into one neighbouring
-    // tile is added atomically to a[v], which edge_init_segsum_fwd zeroed (two partials onto
-    // zero: p + q == q + p, deterministic); one over three or more row tiles (a hub node,
-    // in-degree > BM + 1) leaves its partial in a slot fixed by the data and its last
+    // a[v] = sum_{dst(i) = v} h[i] for the tile's columns (GNN.py:134): the thread owning the
+    // first row of a segment in the tile sums its rows in row order (the segment bounds from the
+    // tile's segment-start mask).  A segment inside the tile is stored; one crossing into one
+    // neighbouring tile is added atomically to a[v], which edge_init_segsum_fwd zeroed (two
+    // partials onto zero: p + q == q + p, deterministic); one over three or more row tiles (a hub
+    // node, in-degree > BM + 1) leaves its partial in a slot fixed by the data and its last
     // contributor sums the slots in row-tile order -- deterministic for every in-degree.
-    // (Measured against one thread per segment head over the apply pass's row mapping: the
-    // chunk walk is 0.9 us faster per launch, profiles/r04_b_*.)
     __syncthreads();
     const int nrow = min(BM, M - m0);
-    constexpr int NCH = BM / 16;
-    for (int q = tid; q < NCH * C4; q += NT) {
-      const int ch = q / C4, c4 = q - ch * C4;
-      const int col = n0 + 4 * c4;
-      if (col >= ep.N) continue;
-      int s = 16 * ch;
-      const int end = min(16 * ch + 16, nrow);
-      if (ch > 0)  // the tail of a segment begun in an earlier chunk belongs to that chunk
-        while (s < end && sd[s + 1] == sd[s]) ++s;
-      while (s < end) {
-        const int v = sd[s + 1];
-        float4 a = f4zero();
-        int r = s;
-        for (; r < nrow && sd[r + 1] == v; ++r)
-          a = f4add(a, *reinterpret_cast<const float4*>(&C[r * S::LDC + 4 * c4]));
-        float* dst = ep.aout + (int64_t)v * ep.lda + col;
-        const bool head = s == 0 && sd[0] == v, tail = r == nrow && sd[nrow + 1] == v;
-        if (tail && !head && ep.znext)  // the tile where a crossing segment starts
-          *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + col) = f4zero();
-        if (head || tail) {
-          const int b = ep.dst_ptr[v], e = ep.dst_ptr[v + 1];
-          if (seg_tiles(b, e, BM) <= 2) {
-            atomicAdd(dst, a.x);
-            atomicAdd(dst + 1, a.y);
-            atomicAdd(dst + 2, a.z);
-            atomicAdd(dst + 3, a.w);
-          } else {
-            sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * c4, a);
-          }
+    const uint64_t mlo = smask[0] | ((uint64_t)smask[1] << 32);
+    const uint64_t mhi = smask[2] | ((uint64_t)smask[3] << 32);
+#pragma unroll
+    for (int it = 0; it < EIT; ++it) {
+      const int r = er0 + RPP * it;
+      if (!eact || r >= nrow || ecol >= ep.N || !seg_bit(mlo, mhi, r)) continue;
+      const int e = seg_end(mlo, mhi, r);
+      const int v = sd[r + 1];
+      float4 a = f4zero();
+      for (int k = r; k < e; ++k)
+        a = f4add(a, *reinterpret_cast<const float4*>(&C[k * S::LDC + 4 * ec4]));
+      float* dst = ep.aout + (int64_t)v * ep.lda + ecol;
+      const bool head = r == 0 && sd[0] == v, tail = e == nrow && sd[nrow + 1] == v;
+      if (tail && !head && ep.znext)  // the tile where a crossing segment starts
+        *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + ecol) = f4zero();
+      if (head || tail) {
+        const int b = ep.dst_ptr[v], ee = ep.dst_ptr[v + 1];
+        if (seg_tiles(b, ee, BM) <= 2) {
+          atomicAdd(dst, a.x);
+          atomicAdd(dst + 1, a.y);
+          atomicAdd(dst + 2, a.z);
+          atomicAdd(dst + 3, a.w);
         } else {
-          *reinterpret_cast<float4*>(dst) = a;
+          sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * ec4, a);
         }
-        s = r;
+      } else {
+        *reinterpret_cast<float4*>(dst) = a;
       }
     }
     // hub segments: the last contributor sums the slots of every row tile in order
