@@ -119,8 +119,10 @@ ArenaLayout arena_layout(const Dims& d) {
   const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
   layout_prefix(d, L, b);
   L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
-  L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
-  L.b3rob = b.take(16 * b3_img_u4(d.H, d.H));
+  // the node-row readout GEMMs in their grid-filling column tiling (b3nt_cols)
+  const B3Cols rc = b3nt_cols((int)d.N, d.H);
+  L.b3rof = b.take(16 * b3_img_u4(rc, d.H));
+  L.b3rob = b.take(16 * b3_img_u4(rc, d.H));
   for (int l = 0; l < d.D; ++l) {
     L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
     L.b3lb[l] = b.take(16 * b3_img_u4(d.H, d.H));
@@ -156,7 +158,7 @@ ArenaLayout eval_arena_layout(const Dims& d) {
   L.g = b.take(4 * B * Hp);
   // forward weight images, packed by every predict that is not handed pre-packed ones
   L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
-  L.b3rof = b.take(16 * b3_img_u4(d.H, d.H));
+  L.b3rof = b.take(16 * b3_img_u4(b3nt_cols((int)d.N, d.H), d.H));
   for (int l = 0; l < d.D; ++l) L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
   L.bytes = b.off;
   L.off_index_begin = 0;

@@ -121,21 +121,24 @@ __device__ __forceinline__ floatx4 b3_mfma6(const b3_u4 (&a)[3], const b3_u4& b0
 struct B3Cols {
   int tiles, nf, nimg;
 };
+// the instantiated fragment counts per tile (launch_b3nt's switch)
+inline int b3_nf_snap(int nf) {
+  static const int sizes[] = {1, 2, 3, 4, 6, 7, 8, 11, 13};
+  for (int s : sizes)
+    if (s >= nf) return s;
+  return 13;
+}
 inline B3Cols b3_cols(int N) {
   const int nft = (N + 15) / 16;
   const int tiles = (nft + 12) / 13;
   int nf = (nft + tiles - 1) / tiles;
-  static const int sizes[] = {1, 2, 3, 4, 6, 8, 11, 13};
-  for (int s : sizes)
-    if (s >= nf) {
-      nf = s;
-      break;
-    }
+  nf = b3_nf_snap(nf);
   return B3Cols{tiles, nf, tiles * nf * 16};
 }
 inline int b3_nk(int K) { return (K + B3_BK - 1) / B3_BK; }
-// b3_u4 elements of an image (3 pieces)
-inline size_t b3_img_u4(int N, int K) { return (size_t)b3_nk(K) * 3 * b3_cols(N).nimg * 4; }
+// b3_u4 elements of an image (3 pieces) in the column tiling c
+inline size_t b3_img_u4(const B3Cols& c, int K) { return (size_t)b3_nk(K) * 3 * c.nimg * 4; }
+inline size_t b3_img_u4(int N, int K) { return b3_img_u4(b3_cols(N), K); }
 
 // one pack job: image rows [n_begin, n_begin + rows) from B(n, k) = src[n * ldn + k * ldk]
 // (n < N real rows of this job, zero beyond; k < K real, zero beyond), times kscale[k] when set
@@ -163,9 +166,12 @@ inline hipError_t b3_pack_add(B3PackJobs& jobs, const B3PackJob& j, hipStream_t 
   return hipSuccess;
 }
 // image job for B(n, k) = src[n * ldn + k * ldk], n < N, k < K, into an image of its own
-inline B3PackJob b3_job(const float* src, int64_t ldn, int64_t ldk, int N, int K, void* img) {
-  const B3Cols c = b3_cols(N);
+inline B3PackJob b3_job(const float* src, int64_t ldn, int64_t ldk, int N, int K, void* img,
+                        const B3Cols& c) {
   return B3PackJob{src, ldn, ldk, static_cast<b3_u4*>(img), 0, c.nimg, N, K, c.nimg, b3_nk(K)};
+}
+inline B3PackJob b3_job(const float* src, int64_t ldn, int64_t ldk, int N, int K, void* img) {
+  return b3_job(src, ldn, ldk, N, K, img, b3_cols(N));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -738,12 +744,44 @@ inline int b3nt_waves(int M, int N) {
 // rows per workgroup tile of launch_b3nt for an M x N GEMM
 inline int b3nt_rows(int M, int N) { return b3nt_waves(M, N) == 8 ? 128 : 64; }
 
-// C = A B^T with B given as its image (b3_pack of the same N, K).  M, N, K > 0.
+// Column tiling of an M-row NT GEMM whose workgroups would leave CUs idle in b3_cols(N)'s tiling
+// (the node-row readout GEMMs of a small batch: 60 row tiles x 2 at cfg2): more, narrower column
+// tiles, chosen by a cost model of waves of workgroups x per-k-step cost, a step costing its
+// MFMAs (nf fragment columns) plus fixed work worth kB3StepFixed columns (A fetch + split, B
+// staging, the barrier: cfg2 layer GEMMs run 1.9 us per 13-column step against 1.3 us of MFMA).
+// Every A row is then loaded and split once per column tile (more A traffic, all L2 hits).
+// Images are packed in the tiling they are launched with (b3_job(..., cols)).
+constexpr int kB3Cus = 256;
+constexpr int kB3StepFixed = 6;
+inline B3Cols b3nt_cols(int M, int N) {
+  const B3Cols c0 = b3_cols(N);
+  const int bm = b3nt_rows(M, N);
+  const int tm = (M + bm - 1) / bm;
+  const int nft = (N + 15) / 16;
+  auto cost = [&](const B3Cols& c) {
+    const int waves = (tm * c.tiles + kB3Cus - 1) / kB3Cus;
+    return waves * (kB3StepFixed + c.nf);
+  };
+  B3Cols best = c0;
+  int bc = cost(c0);
+  for (int nf = c0.nf - 1; nf >= 2; --nf) {
+    if (b3_nf_snap(nf) != nf) continue;
+    const int tiles = (nft + nf - 1) / nf;
+    const B3Cols c{tiles, nf, tiles * nf * 16};
+    const int k = cost(c);
+    if (k < bc) best = c, bc = k;
+  }
+  return best;
+}
+
+// C = A B^T with B given as its image (b3_pack of the same N, K in the column tiling c).
+// M, N, K > 0.
 template <class AL, class EP>
-inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int M, int N, int K,
-                              hipStream_t st) {
+inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const B3Cols& c, const EP& ep,
+                              int M, int N, int K, hipStream_t st) {
   if (M <= 0 || N <= 0) return hipSuccess;
-  const B3Cols c = b3_cols(N);
+  if (c.tiles * c.nf * 16 != c.nimg || c.nimg < N || b3_nf_snap(c.nf) != c.nf)
+    return hipErrorInvalidValue;
   const bool w8 = b3nt_waves(M, N) == 8;
   // unmasked A when K % 4 == 0: every fetched float4 is either all-valid or past K (clamped to
   // finite in-bounds data, multiplied by the image's zero rows)
@@ -761,11 +799,18 @@ inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int
     case 3: return go(std::integral_constant<int, 3>{});
     case 4: return go(std::integral_constant<int, 4>{});
     case 6: return go(std::integral_constant<int, 6>{});
+    case 7: return go(std::integral_constant<int, 7>{});
     case 8: return go(std::integral_constant<int, 8>{});
     case 11: return go(std::integral_constant<int, 11>{});
     case 13: return go(std::integral_constant<int, 13>{});
   }
   return hipErrorInvalidValue;
+}
+// ... in b3_cols(N)'s tiling
+template <class AL, class EP>
+inline hipError_t launch_b3nt(const AL& al, const b3_u4* Bimg, const EP& ep, int M, int N, int K,
+                              hipStream_t st) {
+  return launch_b3nt(al, Bimg, b3_cols(N), ep, M, N, K, st);
 }
 
 }  // namespace cgr

@@ -284,13 +284,14 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     const float* m = d.act == ACT_RELU ? fv.hn : fv.zn;
     const b3_u4* img = static_cast<const b3_u4*>(fv.b3rob);
     const EpStoreRowScale ep{ds, Hp, N, H, dy, iv.node_graph};
+    const B3Cols rc = b3nt_cols(N, H);  // the image's tiling (gnn_fwd.hip)
     // the activation derivative in the A loader, specialised per activation (main-loop code)
     if (d.act == ACT_RELU)
-      HIP_RET(launch_b3nt(LdActGradT<ACT_RELU>{m, Hp, d.act}, img, ep, N, H, H, st));
+      HIP_RET(launch_b3nt(LdActGradT<ACT_RELU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
     else if (d.act == ACT_SILU)
-      HIP_RET(launch_b3nt(LdActGradT<ACT_SILU>{m, Hp, d.act}, img, ep, N, H, H, st));
+      HIP_RET(launch_b3nt(LdActGradT<ACT_SILU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
     else
-      HIP_RET(launch_b3nt(LdActGradT<ACT_GELU>{m, Hp, d.act}, img, ep, N, H, H, st));
+      HIP_RET(launch_b3nt(LdActGradT<ACT_GELU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
   }
 
   // learnable-skip partial-sum slots per layer (bwd_dsig_slots)

@@ -141,14 +141,17 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
                                       H, F, cx.nimg, b3_nk(F)}, side));
     HIP_RET(b3_pack(pj, side));
   }
+  // the readout GEMMs' column tiling: grid-filling over this batch's N rows (b3nt_cols) for the
+  // images packed here, b3_cols(H) for batch-independent caller images (cgr_gnn_pack_images)
+  const B3Cols rcols = caller_images ? b3_cols(H) : b3nt_cols(N, H);
   if (!caller_images) {
     ProfScope _p("weight_pack", st);
     B3PackJobs pm{};
-    HIP_RET(b3_pack_add(pm, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof), st));
+    HIP_RET(b3_pack_add(pm, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof, rcols), st));
     for (int l = 0; l < D; ++l)
       HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l]), st));
     if (!mode.eval && (training & CGR_TRAIN_FOR_BACKWARD)) {  // the backward NT GEMMs' W^T images
-      B3PackJob rob = b3_job(Wn + F, 1, F + H, H, H, fv.b3rob);  // scaled by wf: LdActGrad
+      B3PackJob rob = b3_job(Wn + F, 1, F + H, H, H, fv.b3rob, rcols);  // scaled by wf: LdActGrad
       rob.kscale = params[CGR_PARAM_FFN_W(D)];
       HIP_RET(b3_pack_add(pm, rob, st));
       for (int l = 0; l < D; ++l)
@@ -247,8 +250,8 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   {
     ProfScope _p("gemm_nt_readout_fwd", st);
     EpReadoutQ ep{bn, fv.Q, fv.hn, fv.zn, Hp, N, H, d.act};
-    HIP_RET(launch_b3nt(LdPlain<4>{fv.a[D], Hp}, static_cast<const b3_u4*>(fv.b3rof), ep, N, H, H,
-                        st));
+    HIP_RET(launch_b3nt(LdPlain<4>{fv.a[D], Hp}, static_cast<const b3_u4*>(fv.b3rof), rcols, ep,
+                        N, H, H, st));
   }
   ProfScope _p("pool_head_fwd", st);
   HIP_RET(pool_head_fwd(fv.hn, Hp, iv.graph_ptr, d.B, H, params[CGR_PARAM_FFN_W(D)],
