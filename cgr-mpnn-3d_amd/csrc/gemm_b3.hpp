@@ -216,7 +216,14 @@ struct B3NtShape {
   static constexpr size_t LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
 };
 
-constexpr int B3_LDA = 4;  // B fragment groups read from LDS ahead of the MFMAs that use them
+#ifndef CGR_B3_LDA
+#define CGR_B3_LDA 4
+#endif
+#ifndef CGR_B3_RA_FENCE
+#define CGR_B3_RA_FENCE 1
+#endif
+constexpr int B3_LDA = CGR_B3_LDA;  // B fragment groups read from LDS ahead of the MFMAs using them
+constexpr bool kB3ReadAheadFence = CGR_B3_RA_FENCE;
 
 // Pipeline (one barrier per k step, 3 LDS buffers for B):
 //   iteration ks computes step ks from LDS buffer ks % 3 and A fragments afr[ks & 1], and stages
@@ -336,7 +343,8 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
 #pragma unroll
     for (int j = 0; j < NF; ++j) acc[i][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-  constexpr int LDA = B3_LDA < NF ? B3_LDA : NF - 1;
+  // read-ahead depth: 2 groups at 11 fragment columns (4 spill the gathered-A kernels there)
+  constexpr int LDA = NF == 11 ? 2 : (B3_LDA < NF ? B3_LDA : NF - 1);
   // One step: the MFMAs of step ks (LDS buffer cb, fragments afc), column groups in pairs, with
   // the step's other work spread over them (the vector-memory path and the matrix pipe overlap
   // only when loads are interleaved with the MFMAs; issued as one burst per step they stall every
@@ -369,6 +377,9 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     };
 #pragma unroll
     for (int j = 0; j < LDA; ++j) rd(j);
+    // the read-ahead is issued here, ahead of everything (else the scheduler fills each pair's
+    // ds_read group with that pair's own reads and waits on them right away)
+    if constexpr (kB3ReadAheadFence) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int j = 2 * p;
@@ -458,7 +469,6 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   auto tstep = [&](int cb, const b3_u4 (&afc)[RF][3], const ARaw* xa, b3_u4 (&afn)[RF][3],
                    int ksn, bool prefetch, bool last) {
     const b3_u4* Bs = b3_lds + cb * BU4;
-    constexpr int LDA = B3_LDA < NF ? B3_LDA : NF - 1;
     constexpr int RING = LDA + 2;
     b3_u4 bq[RING][3];
     auto rd = [&](int j) {
@@ -469,6 +479,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     };
 #pragma unroll
     for (int j = 0; j < LDA; ++j) rd(j);
+    if constexpr (kB3ReadAheadFence) __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int j = 2 * p;
