@@ -87,7 +87,9 @@ static void layout_prefix(const Dims& d, ArenaLayout& L, Bump& b) {
   // + the ticket counters of the layer GEMMs' hub segments (EpLayerSeg: zero on entry, reset by
   // each completer)
   L.fcnt = L.status + 16;
-  const size_t fcnt_n = N * (size_t)b3_cols(d.H).tiles;
+  // the layer forward runs in layer_cols(d), or in b3_cols(H) over caller-packed images (predict)
+  const B3Cols lc = layer_cols(d), dc = b3_cols(d.H);
+  const size_t fcnt_n = N * (size_t)std::max(lc.tiles, dc.tiles);
   L.zero_bytes = (size_t)round_up((int64_t)(4 * (4 * N + B) + 16 + 4 * fcnt_n), 16);
   b.take(L.zero_bytes);
   L.rng = b.take(8);
@@ -109,7 +111,9 @@ static void layout_prefix(const Dims& d, ArenaLayout& L, Bump& b) {
   L.Q = b.take(4 * N * Hp);
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
   // partial sums of the layer GEMMs' hub segments (over >= 3 row tiles), one slot pair per tile
-  L.fpart = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)b3_cols(d.H).nf * 16);
+  const size_t rt = (size_t)cdiv(d.E, b3nt_rows((int)d.E, d.H));
+  L.fpart = b.take(4 * rt * 2 * 16 *
+                   std::max((size_t)lc.tiles * lc.nf, (size_t)dc.tiles * dc.nf));
 }
 
 ArenaLayout arena_layout(const Dims& d) {
@@ -118,14 +122,14 @@ ArenaLayout arena_layout(const Dims& d) {
   Bump b;
   const size_t N = (size_t)d.N, E = (size_t)d.E, B = (size_t)d.B, Hp = (size_t)d.Hp;
   layout_prefix(d, L, b);
-  L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
+  L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(b3nt_cols((int)d.N, 2 * d.H), d.F)) : kNone;
   // the node-row readout GEMMs in their grid-filling column tiling (b3nt_cols)
   const B3Cols rc = b3nt_cols((int)d.N, d.H);
   L.b3rof = b.take(16 * b3_img_u4(rc, d.H));
   L.b3rob = b.take(16 * b3_img_u4(rc, d.H));
   for (int l = 0; l < d.D; ++l) {
-    L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
-    L.b3lb[l] = b.take(16 * b3_img_u4(d.H, d.H));
+    L.b3lf[l] = b.take(16 * b3_img_u4(layer_cols(d), d.H));
+    L.b3lb[l] = b.take(16 * b3_img_u4(layer_cols(d), d.H));
   }
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     L.h[l] = l <= d.D ? b.take(4 * E * Hp) : kNone;
@@ -157,9 +161,9 @@ ArenaLayout eval_arena_layout(const Dims& d) {
   L.hn = b.take(4 * N * Hp);
   L.g = b.take(4 * B * Hp);
   // forward weight images, packed by every predict that is not handed pre-packed ones
-  L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(2 * d.H, d.F)) : kNone;
+  L.b3x = d.F > 0 ? b.take(16 * b3_img_u4(b3nt_cols((int)d.N, 2 * d.H), d.F)) : kNone;
   L.b3rof = b.take(16 * b3_img_u4(b3nt_cols((int)d.N, d.H), d.H));
-  for (int l = 0; l < d.D; ++l) L.b3lf[l] = b.take(16 * b3_img_u4(d.H, d.H));
+  for (int l = 0; l < d.D; ++l) L.b3lf[l] = b.take(16 * b3_img_u4(layer_cols(d), d.H));
   L.bytes = b.off;
   L.off_index_begin = 0;
   return L;
@@ -232,9 +236,14 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   return f;
 }
 
+// column tiling of the layer GEMMs (forward and fused backward) over this batch's E rows: b3_cols
+// when that fills the chip, else the narrower tiles of b3nt_cols (small batches: train.py's 32
+// reactions run 60 -> 210 workgroups per layer GEMM)
+B3Cols layer_cols(const Dims& d) { return b3nt_cols((int)d.E, d.H); }
+
 // row tiles x column tiles of the fused layer-backward GEMM (gnn_bwd.hip, ep_bwd.hpp)
 int bwd_seg_tiles(const Dims& d) {
-  return (int)cdiv(d.E, b3nt_rows((int)d.E, d.H)) * b3_cols(d.H).tiles;
+  return (int)cdiv(d.E, b3nt_rows((int)d.E, d.H)) * layer_cols(d).tiles;
 }
 
 // learnable-skip partial sums per layer: the top layer's activation kernel writes one per block,
@@ -293,8 +302,8 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.slab2 = b.take(4 * std::max<size_t>(slab, 1));
   W.bslab2 = b.take(4 * std::max<size_t>(bslab, 1));
   W.dag = b.take(2 * 4 * N * Hp);  // two, alternating by layer
-  W.cnt = b.take(4 * (N * (size_t)b3_cols(d.H).tiles + 1));
-  W.part = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)b3_cols(d.H).nf * 16);
+  W.cnt = b.take(4 * (N * (size_t)layer_cols(d).tiles + 1));
+  W.part = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)layer_cols(d).nf * 16);
   W.dsig_blocks = bwd_dsig_slots(d);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
   W.bytes = b.off;

@@ -298,7 +298,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   const int nb = WL.dsig_blocks;
   // row tile of the fused layer-backward GEMMs: crossing segments accumulate in dag
   const int seg_rows = b3nt_rows(E, H);
-  const int seg_cols = b3_cols(H).tiles;
+  const B3Cols lcols = layer_cols(d);  // the layer images' tiling (gnn_fwd.hip)
+  const int seg_cols = lcols.tiles;
   const int seg_tiles = bwd_seg_tiles(d);
   int* cnt = reinterpret_cast<int*>(ws + WL.cnt);
   float* part = reinterpret_cast<float*>(ws + WL.part);
@@ -375,13 +376,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       float* dg = dag_of(l);
       float* dgn = l > 0 ? dag_of(l - 1) : nullptr;
       if (l > 0)
-        HIP_RET(launch_b3nt(al, img,
+        HIP_RET(launch_b3nt(al, img, lcols,
                             EpLayerBwdSeg<false>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
                                                  iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
                                                  seg_cols},
                             E, H, H, st));
       else
-        HIP_RET(launch_b3nt(al, img,
+        HIP_RET(launch_b3nt(al, img, lcols,
                             EpLayerBwdSeg<true>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
                                                 iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
                                                 seg_cols},

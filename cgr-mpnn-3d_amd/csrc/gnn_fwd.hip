@@ -131,10 +131,12 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   // layer / readout images (forward, and backward unless this is an eval forward) on the caller's
   // stream ahead of graph prep (that chain has slack beside the x-GEMM chain, and the layers
   // that read them run there)
+  // the x-GEMM's column tiling: grid-filling over this batch's N rows for the image packed here
+  const B3Cols xcols = caller_images ? b3_cols(2 * H) : b3nt_cols(N, 2 * H);
   if (F > 0 && !caller_images) {
     ProfScope _p("weight_pack", side);
     B3PackJobs pj{};
-    const B3Cols cx = b3_cols(2 * H);
+    const B3Cols cx = xcols;
     HIP_RET(b3_pack_add(pj, B3PackJob{W0, F + Fe, 1, static_cast<b3_u4*>(fv.b3x), 0, H, H, F,
                                       cx.nimg, b3_nk(F)}, side));
     HIP_RET(b3_pack_add(pj, B3PackJob{Wn, F + H, 1, static_cast<b3_u4*>(fv.b3x), H, cx.nimg - H,
@@ -144,18 +146,21 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   // the readout GEMMs' column tiling: grid-filling over this batch's N rows (b3nt_cols) for the
   // images packed here, b3_cols(H) for batch-independent caller images (cgr_gnn_pack_images)
   const B3Cols rcols = caller_images ? b3_cols(H) : b3nt_cols(N, H);
+  const B3Cols lcols = caller_images ? b3_cols(H) : layer_cols(d);  // the layer GEMMs
   if (!caller_images) {
     ProfScope _p("weight_pack", st);
     B3PackJobs pm{};
     HIP_RET(b3_pack_add(pm, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof, rcols), st));
     for (int l = 0; l < D; ++l)
-      HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l]), st));
+      HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l], lcols),
+                          st));
     if (!mode.eval && (training & CGR_TRAIN_FOR_BACKWARD)) {  // the backward NT GEMMs' W^T images
       B3PackJob rob = b3_job(Wn + F, 1, F + H, H, H, fv.b3rob, rcols);  // scaled by wf: LdActGrad
       rob.kscale = params[CGR_PARAM_FFN_W(D)];
       HIP_RET(b3_pack_add(pm, rob, st));
       for (int l = 0; l < D; ++l)
-        HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l]), st));
+        HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l], lcols),
+                            st));
     }
     HIP_RET(b3_pack(pm, st));
   }
@@ -168,7 +173,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     hipError_t e = with_vec(vec_for(xa, ldx, F), [&](auto VX) {
       LdPlain<decltype(VX)::value> al{xa, ldx};
       EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
-      return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), ep, N, 2 * H, Kx, side);
+      return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), xcols, ep, N, 2 * H, Kx, side);
     });
     HIP_RET(e);
   } else {
@@ -232,14 +237,14 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       // eval ring: a_{l+2} reuses a_{l-1}'s buffer, free once layer l-1 read it; this layer
       // zeroes the entries layer l+1 will accumulate there
       float* znext = (mode.eval && l >= 1 && l + 2 <= D) ? fv.a[l + 2] : nullptr;
-      HIP_RET(launch_b3nt(al, img,
+      HIP_RET(launch_b3nt(al, img, lcols,
                           EpLayerSeg{ep, iv.dst_s, fv.a[l + 1], Hp, znext, iv.dst_ptr, iv.fpart,
-                                     iv.fcnt, b3_cols(H).tiles},
+                                     iv.fcnt, lcols.tiles},
                           E, H, H, st));
     } else {
       {
         ProfScope _p("gemm_nt_layer_fwd", st);
-        HIP_RET(launch_b3nt(al, img, ep, E, H, H, st));
+        HIP_RET(launch_b3nt(al, img, lcols, ep, E, H, H, st));
       }
       ProfScope _p2("segsum_dst_fwd", st);
       HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));

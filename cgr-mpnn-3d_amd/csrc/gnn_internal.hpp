@@ -129,6 +129,8 @@ struct WorkspaceLayout {
 };
 int bwd_dsig_slots(const Dims& d);
 int bwd_seg_tiles(const Dims& d);
+struct B3Cols;
+B3Cols layer_cols(const Dims& d);  // column tiling of the layer GEMMs (capi.hip)
 
 // Forward variants.  Training (cgr_gnn_forward): every activation the backward reads is saved in
 // the arena and the weight images are packed into it by each call.  Eval (cgr_gnn_predict): no
