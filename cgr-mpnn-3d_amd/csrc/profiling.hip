@@ -32,7 +32,10 @@ hipEvent_t get_event() {
     return e;
   }
   hipEvent_t e = nullptr;
-  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  // timing-only events: no system-scope release when recorded, so a bracket measures the launch
+  // and not the write-back of the L2 lines it left dirty (which the default event's release
+  // performs before its timestamp; HIP's own advice for timing events)
+  if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) return nullptr;
   return e;
 }
 }  // namespace
