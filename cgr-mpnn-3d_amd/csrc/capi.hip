@@ -302,7 +302,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.slab2 = b.take(4 * std::max<size_t>(slab, 1));
   W.bslab2 = b.take(4 * std::max<size_t>(bslab, 1));
   W.dag = b.take(2 * 4 * N * Hp);  // two, alternating by layer
-  W.cnt = b.take(4 * (N * (size_t)layer_cols(d).tiles + 1));
+  W.cnt = b.take(4 * (N * (size_t)layer_cols(d).tiles + 2));
   W.part = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)layer_cols(d).nf * 16);
   W.dsig_blocks = bwd_dsig_slots(d);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);

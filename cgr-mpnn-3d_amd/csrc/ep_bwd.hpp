@@ -26,9 +26,14 @@
 // segment's counter; the workgroup that draws the last ticket reads the partial sums and raw rows
 // with sc1 loads (no acquire) and applies the activation backward to all of the segment's rows,
 // then resets the counter and zeroes the segment's entries of the next layer's `dag` buffer (two
-// buffers alternate by layer).  No workgroup waits for another.  Unpaired edge lists (status bit 2) have no such locality: every
-// workgroup stores its rows raw and the last workgroup of the grid runs the src-CSR form over all
-// nodes (correct, slow: a single workgroup -- the CGR edge order is always paired).
+// buffers alternate by layer).  No workgroup waits for another.
+//
+// Unpaired edge lists (status bit 2) have no such locality: every workgroup stores its rows raw
+// and draws a grid ticket; the last K arrivers (K = unpaired_completers(grid) < the CU count)
+// wait until every ticket is drawn -- the others are running or can be dispatched beside the K,
+// so the wait ends -- and complete the src-CSR form over the nodes v = rank (mod K) each, every
+// column.  The last of them to finish resets the two grid counters.  (Round 3 ran it in the grid's
+// last workgroup alone: 6.0 ms per launch at cfg2 against 52 us paired.)
 #pragma once
 
 #include <type_traits>
@@ -39,6 +44,14 @@
 #include "stamps.hpp"
 
 namespace cgr {
+
+// completers of the unpaired form: half the grid, at most half the CUs (the rest of the grid
+// always has CUs to run on while they wait)
+__host__ __device__ inline int unpaired_completers(int grid) {
+  const int k = grid / 2;
+  return k < 1 ? 1 : (k > 128 ? 128 : k);
+}
+constexpr int kUnpairedSpinLimit = 1 << 22;  // ~0.3 s of s_sleep polling, then status bit 16
 
 template <bool EDGE_INIT>
 struct EpLayerBwdSeg {
@@ -53,7 +66,7 @@ struct EpLayerBwdSeg {
   float* dag;          // [nodes, Hp] crossing-segment partial sums of da (zero on entry)
   float* dag_next;     // the next layer's (or null): completed segments' entries zeroed
   float* part;         // [tiles, 2, BN] partials of segments over >= 3 row tiles (slot_of)
-  int* cnt;            // [nodes * tiles_n + 1] tickets (zero on entry, left zero)
+  int* cnt;            // [nodes * tiles_n + 2] tickets (zero on entry, left zero)
   const int* status;   // graph prep's status word
   int M, N, nodes, tiles_n;
 
@@ -145,6 +158,12 @@ struct EpLayerBwdSeg {
     float dsig_c[2] = {0.f, 0.f};  // learnable-skip partials of the segments completed here
     int scratch_f0 = -1, scratch_f1 = -1;
     if (!paired || vh >= 0 || vt >= 0) {  // uniform over the workgroup
+      // unpaired: slot grid + r belongs to completer rank r < K (written once, by it: two
+      // workgroups' plain stores to one slot could land from two XCDs' L2s in either order); the
+      // slots past the completers' are zeroed by their tiles
+      if (!EDGE_INIT && !paired && a.dsig_part && tid == 0 &&
+          tile_id >= unpaired_completers((int)gridDim.x))
+        a.dsig_part[gridDim.x + tile_id] = 0.f;
       ep_vm_drain();  // this wave's partial-sum atomics and raw-row stores
       __syncthreads();
       if (tid == 0) {
@@ -166,9 +185,10 @@ struct EpLayerBwdSeg {
           }
         } else {
           int* gc = cnt + (int64_t)nodes * tiles_n;
+          const int G = (int)gridDim.x, K = unpaired_completers(G);
           const int t = __hip_atomic_fetch_add(gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          any = t == (int)(gridDim.x - 1);
-          scratch[14] = any ? 1 : -1;
+          any = t >= G - K;
+          scratch[14] = any ? t - (G - K) : -1;  // completer rank
           scratch[15] = -1;
         }
         (void)any;
@@ -219,22 +239,48 @@ struct EpLayerBwdSeg {
                 *reinterpret_cast<float4*>(dag_next + gv + n0 + 4 * c4) = f4zero();
           if (tid == 0) cnt[(int64_t)v * tiles_n + tn] = 0;
         }
-      } else if (f0 > 0) {
-        // unpaired: da[v] = sum_{src(e) = v} dm[e] = raw[rev(e)], then every row of v's dst
-        // segment, over all nodes and all columns (this workgroup alone)
+      } else if (f0 >= 0) {
+        // unpaired completer of rank f0: once every workgroup has drawn its ticket (its raw rows
+        // are published), da[v] = sum_{src(e) = v} dm[e] = raw[rev(e)] and every row of v's dst
+        // segment, for the nodes v = f0 (mod K), all columns
+        int* gc = cnt + (int64_t)nodes * tiles_n;
+        const int G = (int)gridDim.x, K = unpaired_completers(G);
+        if (tid == 0) {
+          int spins = 0;
+          while (__hip_atomic_load(gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G &&
+                 ++spins < kUnpairedSpinLimit)
+            __builtin_amdgcn_s_sleep(2);
+          if (spins >= kUnpairedSpinLimit) atomicOr(const_cast<int*>(status), 16);
+        }
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the wait
         const int C4all = a.Hp >> 2;
-        for (int64_t q = tid; q < (int64_t)nodes * C4all; q += NT) {
-          const int v = (int)(q / C4all), col = 4 * (int)(q % C4all);
+        const int64_t mine = nodes > f0 ? (nodes - f0 + K - 1) / K : 0;
+        float ds = 0.f;
+        for (int64_t q = tid; q < mine * C4all; q += NT) {
+          const int v = f0 + K * (int)(q / C4all), col = 4 * (int)(q % C4all);
           float4 da = f4zero();
           for (int j = src_ptr[v], e = src_ptr[v + 1]; j < e; ++j)
             da = f4add(da, sc1_load4(raw + (int64_t)a.rev_s[src_list[j]] * a.Hp + col));
           for (int i = dst_ptr[v], e = dst_ptr[v + 1]; i < e; ++i) {
             const float4 x = sc1_load4(raw + (int64_t)i * a.Hp + col);
-            bwd_row_apply<EDGE_INIT>(a, i, col, f4sub(da, x), key, dsig,
+            bwd_row_apply<EDGE_INIT>(a, i, col, f4sub(da, x), key, ds,
                                      bwd_row_loads<EDGE_INIT>(a, i, col));
           }
         }
-        if (tid == 0) cnt[(int64_t)nodes * tiles_n] = 0;
+        dsig_c[0] = ds;
+        // the last completer to finish resets both grid counters (every completer has passed its
+        // wait by then: it drew its done ticket after it)
+        ep_vm_drain();
+        __syncthreads();
+        if (tid == 0) {
+          const int d = __hip_atomic_fetch_add(gc + 1, 1, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          if (d == K - 1) {
+            gc[0] = 0;
+            gc[1] = 0;
+          }
+        }
       }
     }
 
@@ -267,8 +313,13 @@ struct EpLayerBwdSeg {
           if (tid == 0)
             a.dsig_part[gridDim.x + (dst_ptr[f[k]] / BM) * tiles_n + tn] = sc;
         }
-      const bool starts = paired && vt >= 0 && dst_ptr[vt] >= m0;
-      if (!starts && tid == 0) a.dsig_part[gridDim.x + tile_id] = 0.f;
+      if (paired) {
+        const bool starts = vt >= 0 && dst_ptr[vt] >= m0;
+        if (!starts && tid == 0) a.dsig_part[gridDim.x + tile_id] = 0.f;
+      } else if (f[0] >= 0) {  // unpaired completer: its nodes' partial in the slot of its rank
+        const float sc = block_sum(dsig_c[0]);
+        if (tid == 0) a.dsig_part[gridDim.x + f[0]] = sc;
+      }
     }
   }
 };

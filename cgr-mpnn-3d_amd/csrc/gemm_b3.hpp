@@ -1006,6 +1006,20 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
   constexpr int JB = S::JB;
   extern __shared__ b3_u4 b3_lds[];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
+  CGR_STAMP_BEGIN();
+#ifdef CGR_STAMPS
+  // diagnostic: per step, the cycles a wave works and the cycles it waits at the step barrier, for
+  // compute wave 0 (slots 1, 2) and staging wave 0 (slots 3, 4); slot 5 = main loop end
+  unsigned long long st_work = 0, st_wait = 0, st_prev = 0, st_t = 0;
+  const bool st_me = tid == 0 || tid == CW * 64;
+#define TN_STAMP_PRE() do { if (st_me) { st_t = ::cgr::stamp_now(); st_work += st_t - st_prev; } } while (0)
+#define TN_STAMP_POST() do { if (st_me) { st_prev = ::cgr::stamp_now(); st_wait += st_prev - st_t; } } while (0)
+#define TN_STAMP_START() do { if (st_me) st_prev = ::cgr::stamp_now(); } while (0)
+#else
+#define TN_STAMP_PRE() ((void)0)
+#define TN_STAMP_POST() ((void)0)
+#define TN_STAMP_START() ((void)0)
+#endif
   if (prev.slab) {
     const int64_t tot = reduce_items(prev);
     for (int64_t f = (int64_t)blockIdx.x * S::NT + tid; f < tot; f += (int64_t)gridDim.x * S::NT)
@@ -1092,20 +1106,32 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
       fetch(raw0);  // step 2
       index(3);
       __syncthreads();
+      TN_STAMP_START();
       // interval t (compute on step t): stage step t + 1, whose loads were issued two intervals
       // ago, then issue step t + 3's into the freed set (index loads one interval ahead of them)
       for (int t = 0; t < nt; t += 2) {
         if (t + 1 < nt) stage(raw1, 1);
         fetch(raw1);  // step t + 3
         index(t + 4);
+        TN_STAMP_PRE();
         __syncthreads();
+        TN_STAMP_POST();
         if (t + 1 >= nt) break;
         if (t + 2 < nt) stage(raw0, 0);
         fetch(raw0);  // step t + 4
         index(t + 5);
+        TN_STAMP_PRE();
         __syncthreads();
+        TN_STAMP_POST();
       }
     }
+#ifdef CGR_STAMPS
+    if (tid == CW * 64) {
+      ::cgr::stamp_val(3, st_work);
+      ::cgr::stamp_val(4, st_wait);
+    }
+#endif
+    CGR_STAMP_END(0x4000 | TNN);
     return;
   }
 
@@ -1190,18 +1216,30 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
     b3_u4 a0[NA][2], a1[NA][2];
     aload(0, a0);
     __syncthreads();  // B(0) staged
+    TN_STAMP_START();
     for (int t = 0; t < nt; t += 2) {
       aload(t + 1, a1);
       __builtin_amdgcn_sched_barrier(0);
       compute(0, a0);
+      TN_STAMP_PRE();
       __syncthreads();
+      TN_STAMP_POST();
       if (t + 1 >= nt) break;
       aload(t + 2, a0);
       __builtin_amdgcn_sched_barrier(0);
       compute(1, a1);
+      TN_STAMP_PRE();
       __syncthreads();
+      TN_STAMP_POST();
     }
   }
+#ifdef CGR_STAMPS
+  if (tid == 0) {
+    ::cgr::stamp_val(1, st_work);
+    ::cgr::stamp_val(2, st_wait);
+    ::cgr::stamp_val(5, ::cgr::stamp_now());
+  }
+#endif
 
   // ---- epilogue: accumulators straight to the slab (rows n = 16 nf + 4 fg + r, columns
   // k0 + 16 j + fr: 64 contiguous bytes per row and register) ----
@@ -1234,7 +1272,11 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
       if (own[f] && fg == 0 && n < Nout) bslab[(int64_t)split * Nout + n] = v;
     }
   }
+  CGR_STAMP_END(0x4000 | TNN);
 }
+#undef TN_STAMP_PRE
+#undef TN_STAMP_POST
+#undef TN_STAMP_START
 
 // splits of the e-image TN: rows_per_split a multiple of 32 (plan_b3tn rounds it)
 template <int TNN, int TNK, class BL>
@@ -1244,7 +1286,7 @@ inline hipError_t launch_b3tni_t(const B3EImg& ai, const BL& bl, const B3TnPlan&
   using S = B3TniShape<TNN, TNK>;
   auto kern = gemm_b3tni_kernel<TNN, TNK, BL>;
   static LdsLimit lim;
-  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), 160 * 1024);
+  const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), (int)S::LDS_BYTES);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(kern, dim3(p.tiles_k * p.splits), dim3(S::NT), S::LDS_BYTES, st, ai, bl,
                      slab, bslab, Nout, Kout, R, p.rows_per_split, p.tiles_k, want_bias ? 1 : 0,

@@ -68,6 +68,10 @@ __device__ __forceinline__ void stamp_end(int tag) {
   }
 }
 
+// a value of the caller's into slot i (accumulated cycle counts: gemm_b3tni_kernel)
+__device__ __forceinline__ void stamp_val(int i, unsigned long long v) { stamp_lds()[i] = v; }
+__device__ __forceinline__ unsigned long long stamp_now() { return __builtin_amdgcn_s_memtime(); }
+
 }  // namespace cgr
 
 #define CGR_STAMP_BEGIN() ::cgr::stamp_begin()

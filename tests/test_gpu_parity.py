@@ -671,6 +671,7 @@ def test_unpaired_edge_order_vs_oracle(act, skip, cuda_device):
     assert _pair_status(b, cuda_device) == 0
     assert _pair_status(u, cuda_device) == 4
     _oracle_compare(u, 64, 3, act, skip, cuda_device)
+    _assert_bitwise_reruns(u, 64, 3, skip, cuda_device)
     # a model warns once (its first forward) when the edge order is not reverse-paired
     torch.manual_seed(0)
     for batch, n_warn in ((b, 0), (u, 1)):
@@ -789,3 +790,6 @@ def test_unpaired_edge_order_128_row_tiles_vs_oracle(cuda_device):
     assert u.edge_index.shape[1] >= 96 * 128
     assert _pair_status(u, cuda_device) == 4
     _oracle_compare(u, 48, 2, "relu", True, cuda_device)
+    # the completion is split over the grid's last arrivers (which ones varies run to run); every
+    # node's sums and every learnable-skip partial sit at places fixed by the data
+    _assert_bitwise_reruns(u, 48, 2, True, cuda_device)

@@ -84,6 +84,18 @@ def main():
         rt = (r[:, 3] - r[:, 2]).astype(np.float64) * 10e-3  # us (100 MHz)
         ghz = np.where(rt > 0, cyc / np.maximum(rt, 1e-9) / 1e3, np.nan)
         per_us = 1.0 / (np.nanmedian(ghz) * 1e3)
+        if tag & 0x4000:  # split-bf16 TN (gemm_b3tni_kernel): accumulated cycles, not stamps
+            med = lambda v: round(float(np.median(v)) * per_us, 2)
+            out.append({"tag": "tn", "tnn": tag & 0xFF, "grid": grid,
+                        "t_start_us": round((r[:, 2].min() - t_first) * 1e-2, 2),
+                        "span_us": round((r[:, 3].max() - r[:, 2].min()) * 1e-2, 2),
+                        "wg_life_us": {"med": round(float(np.median(rt)), 2),
+                                       "max": round(float(rt.max()), 2)},
+                        "compute_work_us": med(st[:, 1]), "compute_barrier_wait_us": med(st[:, 2]),
+                        "staging_work_us": med(st[:, 3]), "staging_barrier_wait_us": med(st[:, 4]),
+                        "epilogue_us": med(st[:, 7] - st[:, 5]),
+                        "before_loop_us": med(st[:, 5] - st[:, 0] - st[:, 1] - st[:, 2])})
+            continue
         row = {"tag": tag, "tile": bool(tag & 2), "seg": bool(tag & 1), "nf": (tag >> 2) & 31,
                "waves": tag >> 7, "grid": grid,
                "t_start_us": round((r[:, 2].min() - t_first) * 1e-2, 2),
