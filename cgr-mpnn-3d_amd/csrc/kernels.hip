@@ -308,9 +308,11 @@ hipError_t edge_init_segsum_fwd(const float* P, const int* src_s, const float* e
 // ------------------------------------------------------------------------------------------
 // add-pool + ffn head (GNN.py:110): one workgroup per graph
 // ------------------------------------------------------------------------------------------
-// one workgroup per graph, one thread per float4 column; the node rows of a graph are read 4 at a
-// time (loads issued together, summed in node order)
+// one workgroup per graph, one thread per float4 column; the node rows of a graph are read
+// kPoolBatch at a time (all of a batch's loads issued before its adds, summed in node order: a
+// 30-atom reaction is two round trips instead of eight)
 constexpr int kPoolThreads = 128;
+constexpr int kPoolBatch = 16;
 
 __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restrict__ hn, int Hp,
                                                             const int* __restrict__ gptr, int H,
@@ -325,15 +327,16 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
   for (int c = threadIdx.x; c < C4; c += kPoolThreads) {
     const float* col = hn + 4 * c;
     float4 s = f4zero();
-    int v = v0;
-    for (; v + 4 <= v1; v += 4) {
-      const float4 x0 = *reinterpret_cast<const float4*>(col + (int64_t)v * Hp);
-      const float4 x1 = *reinterpret_cast<const float4*>(col + (int64_t)(v + 1) * Hp);
-      const float4 x2 = *reinterpret_cast<const float4*>(col + (int64_t)(v + 2) * Hp);
-      const float4 x3 = *reinterpret_cast<const float4*>(col + (int64_t)(v + 3) * Hp);
-      s = f4add(f4add(f4add(f4add(s, x0), x1), x2), x3);
+    for (int v = v0; v < v1; v += kPoolBatch) {
+      float4 x[kPoolBatch];
+#pragma unroll
+      for (int u = 0; u < kPoolBatch; ++u)
+        x[u] = v + u < v1 ? *reinterpret_cast<const float4*>(col + (int64_t)(v + u) * Hp)
+                          : f4zero();
+#pragma unroll
+      for (int u = 0; u < kPoolBatch; ++u)
+        if (v + u < v1) s = f4add(s, x[u]);
     }
-    for (; v < v1; ++v) s = f4add(s, *reinterpret_cast<const float4*>(col + (int64_t)v * Hp));
     *reinterpret_cast<float4*>(g + (int64_t)b * Hp + 4 * c) = s;
     const int n = 4 * c;
     const float sv[4] = {s.x, s.y, s.z, s.w};
