@@ -1,6 +1,8 @@
 // Weight images for the split-bf16 NT GEMMs (gemm_b3.hpp): every weight matrix an NT GEMM reads
 // as its B operand is split into three bf16 pieces once per training step (the forward packs
 // W_l, W_l^T, [W0[:, :F]; W_n[:, :F]], W_n[:, F:] and W_n[:, F:]^T in one batched launch).
+#include <algorithm>
+
 #include "gemm_b3.hpp"
 
 namespace cgr {
@@ -40,22 +42,72 @@ __device__ __forceinline__ void b3_pack_job(const B3PackJob& J, int64_t first, i
   }
 }
 
-__global__ __launch_bounds__(256) void k_b3_pack(B3PackJobs jobs) {
-  b3_pack_job(jobs.job[blockIdx.y], (int64_t)blockIdx.x * blockDim.x + threadIdx.x,
-              (int64_t)gridDim.x * blockDim.x);
+// Block ranges of one launch: jobs.n pack jobs of gx blocks each, then the riders' blocks
+// (B3PackRiders: transpose tb, zero fill zb, row padding pb blocks, each grid-strided).
+struct B3PackGrid {
+  int gx, tb, zb, pb;
+};
+
+__global__ __launch_bounds__(256) void k_b3_pack(B3PackJobs jobs, B3PackRiders r, B3PackGrid g) {
+  int b = blockIdx.x;
+  if (b < jobs.n * g.gx) {
+    const int j = b / g.gx;
+    b3_pack_job(jobs.job[j], (int64_t)(b - j * g.gx) * blockDim.x + threadIdx.x,
+                (int64_t)g.gx * blockDim.x);
+    return;
+  }
+  b -= jobs.n * g.gx;
+  if (b < g.tb) {  // rows fastest: adjacent threads write adjacent destination words
+    const int64_t tot = (int64_t)r.t_rows * r.t_cols;
+    for (int64_t t = (int64_t)b * blockDim.x + threadIdx.x; t < tot;
+         t += (int64_t)g.tb * blockDim.x) {
+      const int row = (int)(t % r.t_rows), c = (int)(t / r.t_rows);
+      r.t_dst[(int64_t)c * r.t_ld_dst + row] = r.t_src[(int64_t)row * r.t_ld_src + c];
+    }
+    return;
+  }
+  b -= g.tb;
+  if (b < g.zb) {
+    for (int64_t t = (int64_t)b * blockDim.x + threadIdx.x; t < r.z_u4;
+         t += (int64_t)g.zb * blockDim.x)
+      static_cast<uint4*>(r.z_dst)[t] = make_uint4(0u, 0u, 0u, 0u);
+    return;
+  }
+  b -= g.zb;
+  const int c4n = r.p_ld >> 2;
+  const int64_t tot = r.p_rows * c4n;
+  const bool vec2 = !(r.p_F & 1) && !((uintptr_t)r.p_src & 7);
+  for (int64_t t = (int64_t)b * blockDim.x + threadIdx.x; t < tot; t += (int64_t)g.pb * blockDim.x)
+    pad_row4(r.p_src, r.p_F, r.p_dst, r.p_ld, c4n, t, vec2);
 }
 
-hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st) {
-  if (jobs.n <= 0) return hipSuccess;
-  if (jobs.n > kMaxB3PackJobs) return hipErrorInvalidValue;
+hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st, const B3PackRiders* riders) {
+  if (jobs.n < 0 || jobs.n > kMaxB3PackJobs) return hipErrorInvalidValue;
   int64_t mx = 0;
   for (int i = 0; i < jobs.n; ++i) {
     const int64_t t = (int64_t)jobs.job[i].nk * jobs.job[i].rows * 4;
     mx = t > mx ? t : mx;
   }
-  int gx = (int)((mx + 255) / 256);
-  gx = gx < 1 ? 1 : (gx > 256 ? 256 : gx);
-  hipLaunchKernelGGL(k_b3_pack, dim3(gx, jobs.n), dim3(256), 0, st, jobs);
+  B3PackGrid g{};
+  g.gx = (int)std::min<int64_t>(std::max<int64_t>((mx + 255) / 256, 1), 256);
+  B3PackRiders r{};
+  if (riders) {
+    r = *riders;
+    if (r.t_src && r.t_dst && r.t_rows > 0 && r.t_cols > 0)
+      g.tb = (int)std::min<int64_t>(cdiv((int64_t)r.t_rows * r.t_cols, 256), 64);
+    if (r.z_dst && r.z_u4 > 0) {
+      if ((uintptr_t)r.z_dst & 15) return hipErrorInvalidValue;
+      g.zb = (int)std::min<int64_t>(cdiv(r.z_u4, 256), 256);
+    }
+    if (r.p_src && r.p_dst && r.p_rows > 0) {
+      if ((r.p_ld & 3) || r.p_ld < r.p_F || ((uintptr_t)r.p_dst & 15) || ((uintptr_t)r.p_src & 3))
+        return hipErrorInvalidValue;
+      g.pb = (int)std::min<int64_t>(cdiv(r.p_rows * (r.p_ld >> 2), 256), 2048);
+    }
+  }
+  const int64_t blocks = (int64_t)jobs.n * g.gx + g.tb + g.zb + g.pb;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_b3_pack, dim3((unsigned)blocks), dim3(256), 0, st, jobs, r, g);
   return hipGetLastError();
 }
 

@@ -69,6 +69,26 @@ __device__ __forceinline__ bool drop_keep(uint64_t seed, uint32_t layer, uint64_
 
 __device__ __forceinline__ float4 f4zero() { return make_float4(0.f, 0.f, 0.f, 0.f); }
 
+// float4 t of x rows padded to ldp (c4n = ldp / 4 per row): xp[r, 4k .. 4k + 3] = x[r, 4k ..] or 0
+// past F; vec2: F even and x 8-byte aligned (two 8-byte loads, the float2 past F is zeros)
+__device__ __forceinline__ void pad_row4(const float* __restrict__ x, int F, float* __restrict__ xp,
+                                         int ldp, int c4n, int64_t t, bool vec2) {
+  const int64_t r = t / c4n;
+  const int k = 4 * (int)(t - r * c4n);
+  const float* src = x + r * F;
+  float4 v;
+  if (vec2) {
+    const float2 u = k < F ? *reinterpret_cast<const float2*>(src + k) : make_float2(0.f, 0.f);
+    const float2 w = k + 2 < F ? *reinterpret_cast<const float2*>(src + k + 2) : make_float2(0.f, 0.f);
+    v = make_float4(u.x, u.y, w.x, w.y);
+  } else {
+    v.x = k < F ? src[k] : 0.f;
+    v.y = k + 1 < F ? src[k + 1] : 0.f;
+    v.z = k + 2 < F ? src[k + 2] : 0.f;
+    v.w = k + 3 < F ? src[k + 3] : 0.f;
+  }
+  *reinterpret_cast<float4*>(xp + r * ldp + k) = v;
+}
 __device__ __forceinline__ float4 f4sub(float4 a, float4 b) {
   return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
 }

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "common.hpp"
+#include "prep_one.hpp"
 
 namespace cgr {
 
@@ -225,6 +226,17 @@ struct EpSplit2 {
   float* Q;
   int64_t ld;
   int M, H;
+  // the graph bookkeeping as the launch's extra workgroup when side_on (gemm_b3.hpp kSideBlock,
+  // prep_one.hpp; gnn_fwd.hip decides)
+  static constexpr bool kSideBlock = true;
+  int side_on;
+  PrepOne prep;
+  __device__ __forceinline__ void side(void* lds) const {
+    graph_prep_one(prep, static_cast<int*>(lds));
+  }
+  __host__ __device__ size_t side_lds_bytes() const {
+    return (size_t)prep_one_lds_ints(prep.N, prep.E, prep.B) * 4;
+  }
   __device__ __forceinline__ void apply4(int r, int c, float4 v) const {
     if (r >= M || c >= 2 * H) return;
     if (c + 4 <= H) {

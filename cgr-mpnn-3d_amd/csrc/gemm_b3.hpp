@@ -154,7 +154,25 @@ struct B3PackJobs {
   B3PackJob job[kMaxB3PackJobs];
   int n;
 };
-hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st);
+// small independent jobs that ride in a pack launch (the forward start, gnn_fwd.hip: one launch
+// per queue instead of three); each part is off when its pointer is null
+struct B3PackRiders {
+  // t_dst[c * t_ld_dst + r] = t_src[r * t_ld_src + c], r < t_rows, c < t_cols
+  const float* t_src = nullptr;
+  int64_t t_ld_src = 0;
+  float* t_dst = nullptr;
+  int64_t t_ld_dst = 0;
+  int t_rows = 0, t_cols = 0;
+  // z_u4 16-byte words of zeros at z_dst
+  void* z_dst = nullptr;
+  int64_t z_u4 = 0;
+  // p_dst[r, :p_ld] = p_src[r, :p_F] then zeros, r < p_rows (pad_rows; p_ld % 4 == 0)
+  const float* p_src = nullptr;
+  float* p_dst = nullptr;
+  int64_t p_rows = 0;
+  int p_F = 0, p_ld = 0;
+};
+hipError_t b3_pack(const B3PackJobs& jobs, hipStream_t st, const B3PackRiders* riders = nullptr);
 // append a job, launching the batch when it is full
 inline hipError_t b3_pack_add(B3PackJobs& jobs, const B3PackJob& j, hipStream_t st) {
   if (jobs.n == kMaxB3PackJobs) {
@@ -202,6 +220,22 @@ struct b3_ep_act : std::false_type {};
 template <class EP>
 struct b3_ep_act<EP, std::void_t<decltype(EP::kAct)>> : std::bool_constant<EP::kAct> {};
 
+// epilogue functors with kSideBlock = true may carry one workgroup of independent work (EpSplit2:
+// the graph bookkeeping beside the x-GEMM, prep_one.hpp): when ep.side_on, the launch has one
+// extra, LAST workgroup (the tiles keep their XCD mapping) that runs ep.side(lds) instead of a
+// tile, with the tile's LDS
+template <class EP, class = void>
+struct b3_ep_side : std::false_type {};
+template <class EP>
+struct b3_ep_side<EP, std::void_t<decltype(EP::kSideBlock)>> : std::bool_constant<EP::kSideBlock> {};
+
+// dynamic LDS bytes of a BM x BN NT workgroup (B3NtShape::LDS_BYTES)
+constexpr size_t b3nt_lds_bytes(int BM, int BN) {
+  const size_t stage = (size_t)3 * (3 * BN * 4) * 16;
+  const size_t epi = (size_t)BM * (BN + 4) * 4 + (size_t)(BM + 2) * 4 + 64;
+  return stage > epi ? stage : epi;
+}
+
 template <int WAVES, int RF, int NF>
 struct B3NtShape {
   static constexpr int NT = WAVES * 64;
@@ -214,6 +248,7 @@ struct B3NtShape {
   // scratch (EpLayerBwdSeg; kernels with static LDS cannot be given the full 160 KB dynamically)
   static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4 + 64;
   static constexpr size_t LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
+  static_assert(LDS_BYTES == b3nt_lds_bytes(BM, BN), "b3nt_lds_bytes");
 };
 
 #ifndef CGR_B3_LDA
@@ -243,9 +278,19 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   using S = B3NtShape<WAVES, RF, NF>;
   constexpr int NT = S::NT, BM = S::BM, BN = S::BN, BU4 = S::BU4, BPT = S::BPT;
   extern __shared__ b3_u4 b3_lds[];
+  int nwg = gridDim.x;
+  if constexpr (b3_ep_side<EP>::value) {
+    if (ep.side_on) {
+      if (blockIdx.x == gridDim.x - 1) {
+        ep.side(b3_lds);
+        return;
+      }
+      --nwg;
+    }
+  }
   CGR_STAMP_BEGIN();
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, fr = lane & 15, fg = lane >> 4;
-  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = xcd_remap(blockIdx.x, nwg);
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int nk = (K + B3_BK - 1) / B3_BK;
@@ -740,8 +785,14 @@ inline hipError_t launch_b3nt_t(const AL& al, const b3_u4* Bimg, int nimg, const
   const hipError_t e = lim.ensure(reinterpret_cast<const void*>(kern), (int)S::LDS_BYTES);
   if (e != hipSuccess) return e;
   const int tm = (M + S::BM - 1) / S::BM;
-  hipLaunchKernelGGL(kern, dim3(tm * tiles_n), dim3(WAVES * 64), S::LDS_BYTES, st, al, Bimg, nimg,
-                     ep, M, N, K, tiles_n);
+  int side = 0;
+  if constexpr (b3_ep_side<EP>::value) {
+    side = ep.side_on ? 1 : 0;
+    // the caller checked b3nt_side_fits; a side workgroup needing more LDS than the tile is a bug
+    if (side && ep.side_lds_bytes() > S::LDS_BYTES) return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(kern, dim3(tm * tiles_n + side), dim3(WAVES * 64), S::LDS_BYTES, st, al, Bimg,
+                     nimg, ep, M, N, K, tiles_n);
   return hipGetLastError();
 }
 
@@ -783,6 +834,13 @@ inline B3Cols b3nt_cols(int M, int N) {
     if (k < bc) best = c, bc = k;
   }
   return best;
+}
+
+// whether launch_b3nt(.., c, .., M, N, ..) can host a side workgroup of lds bytes on a CU no tile
+// takes (one NT workgroup per CU: kB3Cus - 1 tiles at most)
+inline bool b3nt_side_fits(int M, int N, const B3Cols& c, size_t lds) {
+  const int bm = b3nt_rows(M, N);
+  return (int64_t)((M + bm - 1) / bm) * c.tiles < kB3Cus && lds <= b3nt_lds_bytes(bm, c.nf * 16);
 }
 
 // C = A B^T with B given as its image (b3_pack of the same N, K in the column tiling c).

@@ -104,52 +104,70 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   SideStreams* ss = side_streams(st);
   if (!ss) return CGR_ERR_HIP;
   std::lock_guard<std::mutex> ss_lock(ss->mu);
+  const bool packs = !caller_images;
+  // column tilings: the x-GEMM's and the readout GEMMs' grid-filling over this batch's N rows
+  // (b3nt_cols) for the images packed here, b3_cols for batch-independent caller images
+  // (cgr_gnn_pack_images); the layer GEMMs' layer_cols
+  const B3Cols xcols = caller_images ? b3_cols(2 * H) : b3nt_cols(N, 2 * H);
+  const B3Cols rcols = caller_images ? b3_cols(H) : b3nt_cols(N, H);
+  const B3Cols lcols = caller_images ? b3_cols(H) : layer_cols(d);
+  // small batches: the graph bookkeeping as the x-GEMM launch's extra workgroup (prep_one.hpp)
+  // on a CU no tile takes -- the whole forward start on one queue, no fork / join (each costs
+  // ~5-10 us in a captured graph); else graph_prep.hip's launches on the caller's stream beside
+  // the x chain on the side stream
+  const bool one_prep =
+      F > 0 && packs && !prep_split() && prep_one_fits(N, E, d.Fep) &&
+      b3nt_side_fits(N, 2 * H, xcols, (size_t)prep_one_lds_ints(N, E, d.B) * 4);
   // instrumented (profiling) runs stay serial so per-kernel event times are isolated durations
-  hipStream_t side = (prof_enabled() || single_stream()) ? st : ss->side;
-  HIP_RET(fork_to(ss, st, side));
+  hipStream_t side = (one_prep || prof_enabled() || single_stream()) ? st : ss->side;
+  if (side != st) HIP_RET(fork_to(ss, st, side));
 
-  // ---- side stream: x padding, x-GEMM image, x-GEMM ----
-  // x rows padded to 16 bytes (F % 4 != 0): the x-GEMM here and both x-part weight gradients
-  // read xp with 16-byte loads
+  // x rows padded to 16 bytes (F % 4 != 0): the x-GEMM and both x-part weight gradients read xp
+  // with 16-byte loads; the padding, W0[:, F:]^T (edge init) and the zeroing of the bookkeeping's
+  // counters ride in the pack launches when this forward packs its own images
   const float* xa = b->x;
   int64_t ldx = F;
+  B3PackRiders rx{}, rm{};
   if (fv.xp) {
-    ProfScope _p("pad_x", side);
-    HIP_RET(pad_rows(b->x, N, F, fv.xp, d.Fp, side));
+    if (packs && F > 0) {
+      rx.p_src = b->x;
+      rx.p_dst = fv.xp;
+      rx.p_rows = N;
+      rx.p_F = F;
+      rx.p_ld = (int)d.Fp;
+    } else {
+      ProfScope _p("pad_x", side);
+      HIP_RET(pad_rows(b->x, N, F, fv.xp, d.Fp, side));
+    }
     xa = fv.xp;
     ldx = d.Fp;
   }
-  // W0[:, F:]^T for the edge init (caller's stream, ahead of graph prep)
-  if (Fe > 0) {
+  if (Fe > 0 && packs) {
+    rm.t_src = W0 + F;
+    rm.t_ld_src = F + Fe;
+    rm.t_dst = fv.w0eT;
+    rm.t_ld_dst = Hp;
+    rm.t_rows = H;
+    rm.t_cols = Fe;
+  } else if (Fe > 0) {
     ProfScope _p("weight_transpose", st);
     TransposeJobs tj{};
     tj.job[0] = TransposeJob{W0, F + Fe, F, fv.w0eT, Hp, H, Fe};
     tj.n = 1;
     HIP_RET(transpose_batch(tj, st));
   }
-  // split-bf16 weight images of every NT GEMM of this step: the x-GEMM's on the side stream; the
-  // layer / readout images (forward, and backward unless this is an eval forward) on the caller's
-  // stream ahead of graph prep (that chain has slack beside the x-GEMM chain, and the layers
-  // that read them run there)
-  // the x-GEMM's column tiling: grid-filling over this batch's N rows for the image packed here
-  const B3Cols xcols = caller_images ? b3_cols(2 * H) : b3nt_cols(N, 2 * H);
-  if (F > 0 && !caller_images) {
-    ProfScope _p("weight_pack", side);
-    B3PackJobs pj{};
-    const B3Cols cx = xcols;
-    HIP_RET(b3_pack_add(pj, B3PackJob{W0, F + Fe, 1, static_cast<b3_u4*>(fv.b3x), 0, H, H, F,
-                                      cx.nimg, b3_nk(F)}, side));
-    HIP_RET(b3_pack_add(pj, B3PackJob{Wn, F + H, 1, static_cast<b3_u4*>(fv.b3x), H, cx.nimg - H,
-                                      H, F, cx.nimg, b3_nk(F)}, side));
-    HIP_RET(b3_pack(pj, side));
-  }
-  // the readout GEMMs' column tiling: grid-filling over this batch's N rows (b3nt_cols) for the
-  // images packed here, b3_cols(H) for batch-independent caller images (cgr_gnn_pack_images)
-  const B3Cols rcols = caller_images ? b3_cols(H) : b3nt_cols(N, H);
-  const B3Cols lcols = caller_images ? b3_cols(H) : layer_cols(d);  // the layer GEMMs
-  if (!caller_images) {
+  // split-bf16 weight images of every NT GEMM of this step: the x-GEMM's on the x chain's
+  // stream, the layer / readout images (forward, and backward unless this is an eval forward) on
+  // the caller's stream ahead of graph prep (one launch when both are the same stream)
+  if (packs) {
     ProfScope _p("weight_pack", st);
-    B3PackJobs pm{};
+    B3PackJobs pj{}, pm{};
+    if (F > 0) {
+      HIP_RET(b3_pack_add(pj, B3PackJob{W0, F + Fe, 1, static_cast<b3_u4*>(fv.b3x), 0, H, H, F,
+                                        xcols.nimg, b3_nk(F)}, side));
+      HIP_RET(b3_pack_add(pj, B3PackJob{Wn, F + H, 1, static_cast<b3_u4*>(fv.b3x), H,
+                                        xcols.nimg - H, H, F, xcols.nimg, b3_nk(F)}, side));
+    }
     HIP_RET(b3_pack_add(pm, b3_job(Wn + F, F + H, 1, H, H, fv.b3rof, rcols), st));
     for (int l = 0; l < D; ++l)
       HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], H, 1, H, H, fv.b3lf[l], lcols),
@@ -162,17 +180,59 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
         HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l], lcols),
                             st));
     }
-    HIP_RET(b3_pack(pm, st));
+    rm.z_dst = iv.zero_block;
+    rm.z_u4 = (int64_t)(iv.zero_bytes / 16);
+    if (side == st) {
+      for (int j = 0; j < pj.n; ++j) HIP_RET(b3_pack_add(pm, pj.job[j], st));
+      rm.p_src = rx.p_src;
+      rm.p_dst = rx.p_dst;
+      rm.p_rows = rx.p_rows;
+      rm.p_F = rx.p_F;
+      rm.p_ld = rx.p_ld;
+    } else {
+      HIP_RET(b3_pack(pj, side, &rx));
+    }
+    HIP_RET(b3_pack(pm, st, &rm));
   }
-  hipEvent_t p_ready = nullptr;  // P and Q written
   if (F > 0) {
     ProfScope _p("gemm_nt_x", side);
     // over padded x the GEMM runs to K = Fp (zero columns against the image's zero rows), the
     // unmasked form, when that adds no k step to the image
     const int Kx = (xa == fv.xp && fv.xp && b3_nk(d.Fp) == b3_nk(F)) ? (int)d.Fp : F;
+    EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
+    if (one_prep) {
+      ep.side_on = 1;
+      PrepOne& po = ep.prep;
+      po.ei = b->edge_index;
+      po.batch = b->batch;
+      po.gptr64 = b->graph_ptr;
+      po.ea = b->edge_attr;
+      po.E = E;
+      po.N = N;
+      po.B = (int)d.B;
+      po.Fe = Fe;
+      po.Fep = (int)d.Fep;
+      po.src_c = iv.src_c;
+      po.dst_c = iv.dst_c;
+      po.perm = iv.perm;
+      po.inv = iv.inv;
+      po.src_s = iv.src_s;
+      po.dst_s = iv.dst_s;
+      po.rev_s = iv.rev_s;
+      po.src_list = iv.src_list;
+      po.dst_ptr = iv.dst_ptr;
+      po.src_ptr = iv.src_ptr;
+      po.graph_ptr = iv.graph_ptr;
+      po.node_graph = iv.node_graph;
+      po.status = iv.status;
+      po.e_s = fv.e_s;
+      po.want_key = any_dropout ? 1 : 0;
+      po.seed = seed;
+      po.counter = rng_counter;
+      po.key_out = iv.rng;
+    }
     hipError_t e = with_vec(vec_for(xa, ldx, F), [&](auto VX) {
       LdPlain<decltype(VX)::value> al{xa, ldx};
-      EpSplit2 ep{fv.P, fv.Q, Hp, N, H};
       return launch_b3nt(al, static_cast<const b3_u4*>(fv.b3x), xcols, ep, N, 2 * H, Kx, side);
     });
     HIP_RET(e);
@@ -180,20 +240,23 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     HIP_RET(hipMemsetAsync(fv.P, 0, sizeof(float) * (size_t)N * Hp, side));
     HIP_RET(hipMemsetAsync(fv.Q, 0, sizeof(float) * (size_t)N * Hp, side));
   }
-  HIP_RET(record_point(ss, side, &p_ready));
-
-  // ---- main stream: graph bookkeeping, then join ----
-  {
-    ProfScope _p("graph_prep", st);
-    PrepArgs pa{b->edge_index, b->batch, b->graph_ptr, b->edge_attr, d.N, d.E, d.B,
-                d.Fe,          d.Fep,   iv,           fv.e_s};
-    pa.want_key = any_dropout;
-    pa.seed = seed;
-    pa.rng_counter = rng_counter;
-    int rc = cgr_graph_prep_impl(pa, st);
-    if (rc) return rc;
+  if (!one_prep) {
+    hipEvent_t p_ready = nullptr;  // P and Q written
+    if (side != st) HIP_RET(record_point(ss, side, &p_ready));
+    // main stream: graph bookkeeping, then join
+    {
+      ProfScope _p("graph_prep", st);
+      PrepArgs pa{b->edge_index, b->batch, b->graph_ptr, b->edge_attr, d.N, d.E, d.B,
+                  d.Fe,          d.Fep,   iv,           fv.e_s};
+      pa.want_key = any_dropout;
+      pa.zeroed = packs;
+      pa.seed = seed;
+      pa.rng_counter = rng_counter;
+      int rc = cgr_graph_prep_impl(pa, st);
+      if (rc) return rc;
+    }
+    if (p_ready) HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
   }
-  HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
 
   // the layer GEMMs sum their dst segments in the epilogue (EpLayerSeg: one gather -> MLP ->
   // segmented-reduce launch per layer) when the fused edge init zeroes what they accumulate

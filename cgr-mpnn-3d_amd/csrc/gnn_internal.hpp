@@ -168,6 +168,8 @@ struct PrepArgs {
   bool want_key = false;
   uint64_t seed = 0;
   uint64_t* rng_counter = nullptr;
+  // idx.zero_block already zeroed on this stream (a pack launch's rider, gnn_fwd.hip)
+  bool zeroed = false;
 };
 
 }  // namespace cgr

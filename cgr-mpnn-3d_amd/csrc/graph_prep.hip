@@ -23,6 +23,7 @@
 // atom in/out-degrees (<= ~10 for molecules), so the per-bucket sort is a few compares.
 #include "common.hpp"
 #include "gnn_internal.hpp"
+#include "prep_one.hpp"
 
 namespace cgr {
 
@@ -133,18 +134,6 @@ __global__ void k_place(const int* __restrict__ key, int n, const int* __restric
   tmp[ptr[k] + slot] = j;
 }
 
-__device__ __forceinline__ void insertion_sort(int* __restrict__ buf, int b, int e) {
-  for (int i = b + 1; i < e; ++i) {
-    const int x = buf[i];
-    int j = i - 1;
-    while (j >= b && buf[j] > x) {
-      buf[j + 1] = buf[j];
-      --j;
-    }
-    buf[j + 1] = x;
-  }
-}
-
 // per bucket insertion sort (ascending) -> stable order
 __global__ void k_bucket_sort(const int* __restrict__ ptr, int nb, int* __restrict__ buf) {
   const int v = blockIdx.x * blockDim.x + threadIdx.x;
@@ -199,7 +188,7 @@ int cgr_graph_prep_impl(const PrepArgs& a, hipStream_t st) {
   const int E = (int)a.E, N = (int)a.N, B = (int)a.B;
   IndexView iv = a.idx;
   // zero counters + status (one contiguous block, see arena layout)
-  HIP_RET(hipMemsetAsync(iv.zero_block, 0, iv.zero_bytes, st));
+  if (!a.zeroed) HIP_RET(hipMemsetAsync(iv.zero_block, 0, iv.zero_bytes, st));
   const int T = 256;
   const int nt = E + N + (a.graph_ptr ? B + 1 : 0);
   hipLaunchKernelGGL(k_prep_count, dim3(cdiv(nt > 0 ? nt : 1, T)), dim3(T), 0, st, a.edge_index,

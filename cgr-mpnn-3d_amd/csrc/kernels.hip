@@ -553,21 +553,7 @@ __global__ __launch_bounds__(256) void k_pad_rows(const float* __restrict__ x, i
   const int c4n = ldp >> 2;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= N * c4n) return;
-  const int64_t r = t / c4n;
-  const int k = 4 * (int)(t - r * c4n);
-  const float* src = x + r * F;
-  float4 v;
-  if (vec2) {  // 8-byte-aligned rows (F even): two 8-byte loads (the float2 past F is zeros)
-    const float2 u = k < F ? *reinterpret_cast<const float2*>(src + k) : make_float2(0.f, 0.f);
-    const float2 w = k + 2 < F ? *reinterpret_cast<const float2*>(src + k + 2) : make_float2(0.f, 0.f);
-    v = make_float4(u.x, u.y, w.x, w.y);
-  } else {
-    v.x = k < F ? src[k] : 0.f;
-    v.y = k + 1 < F ? src[k + 1] : 0.f;
-    v.z = k + 2 < F ? src[k + 2] : 0.f;
-    v.w = k + 3 < F ? src[k + 3] : 0.f;
-  }
-  *reinterpret_cast<float4*>(xp + r * ldp + k) = v;
+  pad_row4(x, F, xp, ldp, c4n, t, vec2 != 0);
 }
 
 hipError_t pad_rows(const float* x, int64_t N, int F, float* xp, int ldp, hipStream_t st) {

@@ -22,6 +22,11 @@ bool single_stream() {
   return on;
 }
 
+bool prep_split() {
+  const char* v = getenv("CGR_PREP_SPLIT");
+  return v && v[0] == '1';
+}
+
 // Keyed by the device of the caller's stream (the null stream: the current device).  The side
 // stream and its events are created on that device, whatever device is current.  The event ring
 // is per device; its users hold SideStreams::mu across each forward / backward enqueue, so

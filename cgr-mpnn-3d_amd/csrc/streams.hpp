@@ -23,6 +23,9 @@ struct SideStreams {
 // CGR_SINGLE_STREAM=1 in the environment: everything on the caller's stream (A/B of the
 // side-stream concurrency against the cross-queue dependency latency it adds in a graph)
 bool single_stream();
+// CGR_PREP_SPLIT=1 (read per call; tests): the graph bookkeeping always as its own launches
+// (graph_prep.hip), never as the x-GEMM's side workgroup (prep_one.hpp)
+bool prep_split();
 
 // returns nullptr and sets the library error if the streams cannot be created
 SideStreams* side_streams(hipStream_t main);

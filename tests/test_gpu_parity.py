@@ -117,20 +117,30 @@ def _graph_prep_check(b, dev, use_ptr=True, batch_none=False):
     assert not es[:, Fe:].any()
 
 
-def test_graph_prep_bit_exact_cfg2(cuda_device):
+# split: graph_prep.hip's launches (CGR_PREP_SPLIT=1) instead of the x-GEMM launch's side
+# workgroup (prep_one.hpp), which every batch small enough takes by default
+@pytest.mark.parametrize("split", [False, True])
+def test_graph_prep_bit_exact_cfg2(split, cuda_device, monkeypatch):
+    monkeypatch.setenv("CGR_PREP_SPLIT", "1" if split else "0")
     _graph_prep_check(make_batch(256, seed=1234), cuda_device)
 
 
-def test_graph_prep_bit_exact_ragged_batch_vector_only(cuda_device):
+@pytest.mark.parametrize("split", [False, True])
+def test_graph_prep_bit_exact_ragged_batch_vector_only(split, cuda_device, monkeypatch):
+    monkeypatch.setenv("CGR_PREP_SPLIT", "1" if split else "0")
     _graph_prep_check(make_batch(37, n_atoms=25, n_bonds=30, n_mace=0, seed=5, n_atoms_jitter=20),
                       cuda_device, use_ptr=False)
 
 
-def test_graph_prep_bit_exact_stress_graphs(cuda_device):
+@pytest.mark.parametrize("split", [False, True])
+def test_graph_prep_bit_exact_stress_graphs(split, cuda_device, monkeypatch):
+    monkeypatch.setenv("CGR_PREP_SPLIT", "1" if split else "0")
     _graph_prep_check(make_batch(8, n_atoms=200, n_bonds=400, n_mace=0, seed=6), cuda_device)
 
 
-def test_graph_prep_single_graph_batch_none(cuda_device):
+@pytest.mark.parametrize("split", [False, True])
+def test_graph_prep_single_graph_batch_none(split, cuda_device, monkeypatch):
+    monkeypatch.setenv("CGR_PREP_SPLIT", "1" if split else "0")
     _graph_prep_check(make_batch(1, n_atoms=10, n_bonds=12, n_mace=0, seed=7), cuda_device,
                       batch_none=True)
 
@@ -399,7 +409,9 @@ def test_last_graph_isolated_node_strict_mode(cuda_device):
     assert torch.isfinite(y).all()
 
 
-def test_out_of_range_edge_index_reported_in_strict_mode(cuda_device):
+@pytest.mark.parametrize("split", [False, True])
+def test_out_of_range_edge_index_reported_in_strict_mode(split, cuda_device, monkeypatch):
+    monkeypatch.setenv("CGR_PREP_SPLIT", "1" if split else "0")
     from cgr_mpnn_3D._amd import config
 
     b = make_batch(3, n_atoms=8, n_bonds=8, n_mace=0, seed=3)
@@ -655,7 +667,7 @@ def _pair_status(b, dev):
 
 
 @pytest.mark.parametrize("act,skip", [("relu", True), ("gelu", False)])
-def test_unpaired_edge_order_vs_oracle(act, skip, cuda_device):
+def test_unpaired_edge_order_vs_oracle(act, skip, cuda_device, monkeypatch):
     # edges shuffled inside every graph: e ^ 1 is no longer the reverse of e, and the reference
     # still pairs them positionally (flip of view(E/2, 2, H), GNN.py:136-138).  Graph prep flags
     # it (status bit 2) and the backward's fused src sum takes its src-CSR form instead of the
@@ -668,8 +680,10 @@ def test_unpaired_edge_order_vs_oracle(act, skip, cuda_device):
     order = np.concatenate([g * per + rng.permutation(per) for g in range(b.num_graphs)])
     u = replace(b, edge_index=np.ascontiguousarray(b.edge_index[:, order]),
                 edge_attr=np.ascontiguousarray(b.edge_attr[order]))
-    assert _pair_status(b, cuda_device) == 0
-    assert _pair_status(u, cuda_device) == 4
+    for split in ("1", "0"):  # both graph-prep forms (test_graph_prep_bit_exact_*)
+        monkeypatch.setenv("CGR_PREP_SPLIT", split)
+        assert _pair_status(b, cuda_device) == 0
+        assert _pair_status(u, cuda_device) == 4
     _oracle_compare(u, 64, 3, act, skip, cuda_device)
     _assert_bitwise_reruns(u, 64, 3, skip, cuda_device)
     # a model warns once (its first forward) when the edge order is not reverse-paired
