@@ -40,7 +40,8 @@ inline void clear_stale_hip_error() { (void)hipGetLastError(); }
 
 // Index bookkeeping inside the arena (all int32).
 struct IndexView {
-  // zero block (memset each call): deg_dst, deg_src, cursor, cursor2, graph_cnt, status
+  // zero block (zeroed each forward: a rider of the pack launch, or a memset with caller images):
+  // deg_dst, deg_src, cursor, cursor2, graph_cnt, status, fcnt
   int* deg_dst;
   int* deg_src;
   int* cursor;
