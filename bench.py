@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="cfg2",
-                    choices=["cfg1", "cfg2", "cfg4", "cfg5", "train_default"])
+                    choices=["cfg1", "cfg2", "cfg4", "cfg5", "train_default", "sweep_b16",
+                             "sweep_b64"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a HIP graph (1/0; -1 = auto: on for N = 1)")
     ap.add_argument("--loss", default="fused", choices=["fused", "torch"],
@@ -335,6 +336,34 @@ def inference_measurement(model, data, B, dev, steps=50):
 
 
 # ------------------------------------------------------------------------------------------------
+def host_cpu_info():
+    """What the CPU baseline ran on: the CPU model, the machine's physical cores and logical
+    CPUs, the CPUs this process may run on, and the torch intra-op threads the baseline used
+    (`cores` of the cpu_baseline object = those threads)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        import psutil
+
+        phys, logical = psutil.cpu_count(logical=False), psutil.cpu_count(logical=True)
+    except Exception:  # noqa: BLE001
+        phys, logical = None, os.cpu_count()
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = None
+    return {"cpu_model": model, "machine_physical_cores": phys, "machine_logical_cpus": logical,
+            "process_allowed_cpus": allowed, "torch_threads": torch.get_num_threads(),
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
 def cpu_baseline(cfgname, seconds, dropout):
     """Reference CPU path (oracle/dmpnn_torch.py: the reference ATen op sequence incl. its dead
     readout GEMM) on this host's cores: same batch shape, MSE(sum) + backward + Adam(amsgrad)."""
@@ -373,7 +402,7 @@ def cpu_baseline(cfgname, seconds, dropout):
         if el >= seconds or n >= 200:
             break
     return {"value": round(n * b.num_graphs / el, 2), "unit": "reactions/s",
-            "cores": torch.get_num_threads(), "kind": "port",
+            "cores": torch.get_num_threads(), "kind": "port", "host": host_cpu_info(),
             "sample": f"{n} training steps of the {cfgname} batch ({b.num_graphs} reactions, "
                       f"fwd+MSE+bwd+Adam) with the torch-CPU restatement of the reference op "
                       f"sequence, {el:.1f} s, torch {torch.__version__}, "
@@ -396,6 +425,10 @@ def main():
     dev = torch.device("cuda", ordinal)
     distributed = world > 1 or bool(args.force_dist)
     if distributed:
+        # an abort on a runtime thread (RCCL / HIP / c10d) prints its native stack
+        from cgr_mpnn_3D._amd import native as _native
+
+        _native.load().cgr_debug_abort_backtrace(1)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
         os.environ.setdefault("RANK", str(rank))
@@ -492,7 +525,11 @@ def main():
     roof_scatter = None
     roof_all = {}
     breakdown = {}
-    if args.profile_steps > 0:
+    # gloo rehearsal (several ranks on one GPU, host-staged collectives): the instrumented pass
+    # would time kernels queued behind other ranks' work and gloo's host copies -- meaningless
+    # per-kernel durations, so the line carries no roofline then
+    gloo_rehearsal = distributed and args.dist_backend == "gloo"
+    if args.profile_steps > 0 and not gloo_rehearsal:
         lib.cgr_profile_reset()
         lib.cgr_profile_enable(1)
         for _ in range(args.profile_steps):
@@ -590,6 +627,9 @@ def main():
                             + (", HIP-graph captured" if args.graph else ""),
                 "global_batch": world * B, "parallelism": f"dp{world}"},
             "roofline": roof, "roofline_scatter_add": roof_scatter,
+            "roofline_note": ("omitted: gloo rehearsal (ranks share one GPU; the instrumented "
+                              "pass would time other ranks' work and gloo's host copies)")
+            if gloo_rehearsal else None,
             "roofline_frac_by_class": roof_all, "kernel_breakdown": breakdown,
             "cpu_baseline": cpu,
         }

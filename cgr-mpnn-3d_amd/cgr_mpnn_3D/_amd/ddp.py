@@ -18,8 +18,6 @@ per-rank gradients reproduces the single-process gradient of the whole global ba
 
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -59,13 +57,10 @@ class GradAllReduce:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def close(self):
-        """Synchronise and drop the communication streams and bucket events (teardown, before
-        ``dist.destroy_process_group``: see ``teardown``)."""
-        for st in self._streams.values():
-            st.synchronize()
-        for evs in self._events.values():
-            for e in evs:
-                e.synchronize()
+        """Drop the communication streams and bucket events (teardown, before
+        ``dist.destroy_process_group``: see ``teardown``).  The caller has synchronised the
+        device; no event is queried or synchronised here -- after a capture the events' last
+        records live in a graph, and a host wait on them is not meaningful."""
         self._streams.clear()
         self._events.clear()
 
@@ -100,59 +95,40 @@ def remove_grad_allreduce(model):
     return model
 
 
-def _collect_verbosely():
-    """Diagnostic (CGR_TEARDOWN_DIAG=1): free the collector's garbage one object at a time,
-    naming each on stderr first, so an abort inside the collection names its object."""
-    import gc
-    import sys
-
-    gc.set_debug(gc.DEBUG_SAVEALL)
-    gc.collect()
-    gc.set_debug(0)
-    junk = list(gc.garbage)
-    gc.garbage.clear()
-    print(f"[teardown] {len(junk)} collectable objects", file=sys.stderr, flush=True)
-    while junk:
-        o = junk.pop()
-        t = type(o)
-        if "torch" in t.__module__ or "cgr" in t.__module__ or t.__name__ in ("Event", "Stream"):
-            print(f"[teardown] freeing {t.__module__}.{t.__qualname__}", file=sys.stderr,
-                  flush=True)
-        del o
-        gc.collect()
-    print("[teardown] garbage freed", file=sys.stderr, flush=True)
-
-
 def teardown(model=None):
-    """End data parallelism in the order the communicator needs, then destroy the process group.
+    """End data parallelism in a fixed order that depends on no garbage collection, then destroy
+    the process group.
 
-    A collective captured into a HIP graph leaves RCCL state tied to that graph: RCCL attaches a
-    destructor (a graph user object, ``hipGraphRetainUserObject``) that hands the captured
-    collective's launch plan back to its communicator when the graph is destroyed.  Destroying
-    the communicator while such a graph is alive -- what ``bench.py`` did (round 3: the captured
-    step ``g`` was still referenced at ``destroy_process_group``) -- lets that destructor run
-    against a freed communicator later, at interpreter exit: an intermittent abort after all the
-    work had succeeded.  So, in this order: the caller drops every captured graph that recorded a
-    collective (and any bound ``g.replay``) BEFORE calling this; here the device is synchronised,
-    reference cycles are collected (the graph destructors run now, while the communicator lives),
-    the device is synchronised again, the gradient hook's communication streams and events are
-    released, the ranks meet at a barrier and only then is the process group destroyed."""
+    Order: (1) the caller drops every captured graph that recorded a collective (and any bound
+    ``g.replay``) BEFORE calling this -- a captured collective leaves RCCL state tied to its graph
+    (a graph user object, ``hipGraphRetainUserObject``, that hands the captured launch plan back
+    to the communicator when the graph is destroyed), so those graphs must die while the
+    communicator lives (round 3 destroyed the communicator first and aborted at interpreter
+    exit); (2) the device is synchronised; (3) the gradient hook's streams and events are dropped
+    (``GradAllReduce.close``) and the device synchronised again; (4) the ranks meet at a barrier;
+    (5) the process group is destroyed; (6) only then is garbage collected.
+
+    No collection runs while the communicator is alive (round 4 collected here, between (2) and
+    (3)).  A captured step leaves no graph, event or tensor in a reference cycle
+    (``tools/rccl_teardown_probe.py``: the collector finds only ctypes type objects after it), so
+    a collection at that point freed nothing of this process group's and only re-ordered the
+    release of EARLIER work's objects against the communicator's own threads -- which is where
+    the one round-4 abort struck (on a native thread, not in a destructor the
+    collector ran).  ``cgr_debug_abort_backtrace`` prints the native stack of any such abort."""
     import gc
 
     if not dist.is_initialized():
         return
     if torch.cuda.is_available():
         torch.cuda.synchronize()
-    if os.environ.get("CGR_TEARDOWN_DIAG") == "1":
-        _collect_verbosely()
-    gc.collect()
-    if torch.cuda.is_available():
-        torch.cuda.synchronize()
     if model is not None:
         remove_grad_allreduce(model)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
     if dist.get_world_size() > 1:
         dist.barrier()
     dist.destroy_process_group()
+    gc.collect()
 
 
 def shard_ranges(graph_edges: np.ndarray, world: int) -> list[tuple[int, int]]:

@@ -74,7 +74,8 @@ def grad_layout(shapes, depth):
 
 def read_status(arena, cfg, N, E, B) -> int:
     """Graph-prep status word (bit0 bad edge index, bit1 bad/unsorted batch, bit2 edges not
-    reverse-paired: informational).  Synchronises."""
+    reverse-paired: informational, bit4 the unpaired backward's completion timed out).
+    Synchronises."""
     lib = native.load()
     off = lib.cgr_gnn_arena_offset(ctypes.byref(cfg), N, E, B, b"status", 0)
     return int(arena[off:off + 4].view(torch.int32).item())
@@ -123,6 +124,7 @@ class GNNFunction(torch.autograd.Function):
     def backward(ctx, dy):
         lib = native.load()
         x, edge_index, edge_attr, batch, graph_ptr, arena, *params = ctx.saved_tensors
+        native.raise_device_errors(x.device, clear=False)  # an earlier backward's timeout
         cfg = make_config(*ctx.cfg_tuple)
         N, E, B = int(x.shape[0]), int(edge_index.shape[1]), ctx.num_graphs
         dev = x.device
@@ -191,6 +193,9 @@ def raise_on_status(arena, cfg, N, E, B, predict=False):
         raise IndexError("cgr_mpnn_3D: edge_index holds a node id outside [0, num_nodes)")
     if st & 2:
         raise RuntimeError("cgr_mpnn_3D: batch vector is not sorted / out of range")
+    if st & 16:
+        raise RuntimeError("cgr_mpnn_3D: the unpaired-edge backward's completion timed out "
+                           "(gradients NaN-poisoned, ep_bwd.hpp)")
 
 
 def gnn_forward(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, dropout_ps,

@@ -15,7 +15,7 @@ _LIB_NAME = "libcgr_mpnn3d.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CGR_MPNN3D_LIB", os.path.join(_HERE, "lib", _LIB_NAME))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 TRAIN_DROPOUT, TRAIN_FOR_BACKWARD = 1, 2  # cgr_gnn_forward / _backward `training` bits
 MAX_DEPTH = 32
 ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
@@ -109,7 +109,11 @@ SIGNATURES = [
     ("cgr_profile_reset", None, []),
     ("cgr_profile_report", c_int64, [c_char_p, c_int64]),
     ("cgr_debug_stamps", c_int32, [c_void_p, c_int64]),
+    ("cgr_device_errors", c_int32, [c_int32, c_int32]),
+    ("cgr_debug_abort_backtrace", c_int32, [c_int32]),
 ]
+
+DEVERR_UNPAIRED_SEEN, DEVERR_UNPAIRED_TIMEOUT = 4, 16  # cgr_device_errors bits
 
 _lib = None
 _load_error: Exception | None = None
@@ -178,3 +182,19 @@ def profile_report() -> dict:
         name, cnt, ms = line.split()
         out[name] = (int(cnt), float(ms))
     return out
+
+
+def raise_device_errors(device, clear: bool = True):
+    """Raise if a kernel of `device` reported an error condition (cgr_device_errors: pinned host
+    memory, no device sync).  Conditions surface once their kernel has run -- at the next native
+    call of the model, or right away after a synchronize.  Returns the informational bits."""
+    import torch
+
+    idx = device.index if getattr(device, "index", None) is not None else \
+        torch.cuda.current_device()
+    bits = int(load().cgr_device_errors(int(idx), 1 if clear else 0))
+    if bits & DEVERR_UNPAIRED_TIMEOUT:
+        raise RuntimeError(
+            "cgr_mpnn_3D: the unpaired-edge backward's completion timed out on "
+            f"cuda:{idx}; the gradients of that backward are NaN-poisoned (ep_bwd.hpp)")
+    return bits

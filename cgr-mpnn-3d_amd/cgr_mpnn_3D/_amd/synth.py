@@ -190,4 +190,10 @@ CONFIGS = {
     # batch size 32 (train.py:209), CGR + MACE features
     "train_default": dict(num_graphs=32, n_atoms=30, n_bonds=30, n_mace=768, depth=3, hidden=300,
                           learnable_skip=False),
+    # the sweep's other batch sizes (hyperparameter_study/sweep_config.json:12: 16 / 32 / 64) at
+    # train.py's default model
+    "sweep_b16": dict(num_graphs=16, n_atoms=30, n_bonds=30, n_mace=768, depth=3, hidden=300,
+                      learnable_skip=False),
+    "sweep_b64": dict(num_graphs=64, n_atoms=30, n_bonds=30, n_mace=768, depth=3, hidden=300,
+                      learnable_skip=False),
 }

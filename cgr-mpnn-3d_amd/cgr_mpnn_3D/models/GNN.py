@@ -53,25 +53,32 @@ def _activation_code(fn) -> int:
         "F.relu, F.silu, F.gelu (train.py:284-292)")
 
 
+_UNPAIRED_MSG = (
+    "cgr_mpnn_3D: edge_index is not reverse-paired (edge 2k+1 is not the reverse of edge 2k, as "
+    "the CGR featuriser emits them, graph_features.py:184-195); results follow the reference's "
+    "positional pairing exactly, but the native layer backward then stores every dm row and "
+    "completes da = segsum_src(dm) in the last 16 workgroups of each launch (ep_bwd.hpp), several "
+    "times slower per layer")
+
+
 def _warn_if_unpaired(edge_index):
-    """Once per module (its first forward; one device sync): warn when edge 2k+1 is not the
-    reverse of edge 2k.  The reference pairs e with e ^ 1 positionally whatever they hold
-    (flip(view(E/2, 2, H)), GNN.py:136-138) and so does the native path, so results stay exact;
-    but the CGR featuriser always emits (a, b), (b, a) pairs (graph_features.py:184-195), and
-    the fused layer backward's fast form relies on it -- unpaired input takes its grid-wide
-    last-workgroup form (ep_bwd.hpp), many times slower."""
+    """A module's first forward (one device sync): warn when edge 2k+1 is not the reverse of edge
+    2k.  The reference pairs e with e ^ 1 positionally whatever they hold (flip(view(E/2, 2, H)),
+    GNN.py:136-138) and so does the native path, so results stay exact; but the CGR featuriser
+    always emits (a, b), (b, a) pairs (graph_features.py:184-195), and the fused layer
+    backward's fast form relies on it.  Later batches are covered without a sync: the unpaired
+    backward reports itself through the device's error words (cgr_device_errors), which every
+    forward reads."""
     import warnings
 
     e = edge_index
     if e.shape[1] < 2:
-        return
+        return False
     bad = (e[0, 1::2] != e[1, 0::2]) | (e[1, 1::2] != e[0, 0::2])
     if bool(bad.any()):
-        warnings.warn(
-            "cgr_mpnn_3D: edge_index is not reverse-paired (edge 2k+1 is not the reverse of edge "
-            "2k, as the CGR featuriser emits them, graph_features.py:184-195); results follow "
-            "the reference's positional pairing exactly, but the native backward takes a slow "
-            "single-workgroup form", RuntimeWarning, stacklevel=3)
+        warnings.warn(_UNPAIRED_MSG, RuntimeWarning, stacklevel=3)
+        return True
+    return False
 
 
 class GNN(nn.Module):
@@ -221,10 +228,19 @@ class GNN(nn.Module):
             raise RuntimeError(
                 "Sizes of tensors must match: scatter size max(edge_index[1])+1 != num_nodes")
 
+        # kernel-reported conditions (no sync): an unpaired backward's completion that timed out
+        # raises here; an unpaired batch seen by any earlier backward warns once per module
+        if native.raise_device_errors(dev) & native.DEVERR_UNPAIRED_SEEN and \
+                not getattr(self, "_cgr_unpaired_warned", False):
+            import warnings
+
+            self._cgr_unpaired_warned = True
+            warnings.warn(_UNPAIRED_MSG, RuntimeWarning, stacklevel=2)
         if not getattr(self, "_cgr_pairing_checked", False) and \
                 not torch.cuda.is_current_stream_capturing():
             self._cgr_pairing_checked = True
-            _warn_if_unpaired(edge_index)
+            if not getattr(self, "_cgr_unpaired_warned", False) and _warn_if_unpaired(edge_index):
+                self._cgr_unpaired_warned = True
 
         params = self.native_parameters()
         for p in params:

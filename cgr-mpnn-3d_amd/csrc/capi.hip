@@ -8,8 +8,10 @@
 #include <unordered_map>
 
 #include "dispatch.hpp"
+#include "ep_bwd.hpp"
 #include "gnn_internal.hpp"
 #include "kernels.hpp"
+#include "streams.hpp"
 
 namespace cgr {
 
@@ -302,7 +304,8 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.slab2 = b.take(4 * std::max<size_t>(slab, 1));
   W.bslab2 = b.take(4 * std::max<size_t>(bslab, 1));
   W.dag = b.take(2 * 4 * N * Hp);  // two, alternating by layer
-  W.cnt = b.take(4 * (N * (size_t)layer_cols(d).tiles + 2));
+  // segment tickets, then one unpaired grid counter per fused layer-backward launch
+  W.cnt = b.take(4 * (N * (size_t)layer_cols(d).tiles + CGR_MAX_DEPTH));
   W.part = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)layer_cols(d).nf * 16);
   W.dsig_blocks = bwd_dsig_slots(d);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
@@ -506,6 +509,20 @@ int cgr_gnn_predict(const cgr_gnn_config* cfg, const float* const* params, const
   note_forward(arena, -1);  // never a backward's arena
   return gnn_forward_impl(d, params, b, dropout_p, seed, rng_counter, training, arena, y,
                           (hipStream_t)stream, m);
+}
+
+int32_t cgr_device_errors(int32_t device, int32_t clear) {
+  SideStreams* ss = side_streams_of(device);
+  if (!ss || !ss->err_host) return 0;
+  volatile int* w = ss->err_host;
+  int32_t bits = 0;
+  if (w[kDevErrUnpairedTimeout]) bits |= CGR_DEVERR_UNPAIRED_TIMEOUT;
+  if (w[kDevErrUnpairedSeen]) bits |= CGR_DEVERR_UNPAIRED_SEEN;
+  if (clear) {
+    if (bits & CGR_DEVERR_UNPAIRED_TIMEOUT) w[kDevErrUnpairedTimeout] = 0;
+    if (bits & CGR_DEVERR_UNPAIRED_SEEN) w[kDevErrUnpairedSeen] = 0;
+  }
+  return bits;
 }
 
 int cgr_segment_sum(const float* values, int64_t ld_values, const int32_t* index,

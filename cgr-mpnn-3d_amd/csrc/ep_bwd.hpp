@@ -29,11 +29,18 @@
 // buffers alternate by layer).  No workgroup waits for another.
 //
 // Unpaired edge lists (status bit 2) have no such locality: every workgroup stores its rows raw
-// and draws a grid ticket; the last K arrivers (K = unpaired_completers(grid) < the CU count)
-// wait until every ticket is drawn -- the others are running or can be dispatched beside the K,
-// so the wait ends -- and complete the src-CSR form over the nodes v = rank (mod K) each, every
-// column.  The last of them to finish resets the two grid counters.  (Round 3 ran it in the grid's
-// last workgroup alone: 6.0 ms per launch at cfg2 against 52 us paired.)
+// and draws a ticket from this launch's own grid counter (one per fused launch, all zeroed by the
+// top layer's activation kernel; nothing resets them mid-backward, so one launch's counts can
+// never leak into the next); the last K arrivers (K = unpaired_completers(grid) <= 16) wait
+// until every ticket is drawn and complete the src-CSR form over the nodes v = rank (mod K),
+// every column.  The wait always ends: workgroups are dispatched round-robin over the 8 XCDs of
+// 32 CUs, so K <= 16 spinning workgroups can never hold every CU of any XCD, and every other
+// workgroup (of this launch or of a kernel beside it) runs to its end without waiting -- a CU of
+// the XCD an undispatched workgroup belongs to always frees up.  Should a wait still exceed the
+// spin limit, the completer reports it (status bit 16, and the host-visible error word the
+// Python side raises from: cgr_device_errors) and writes NaN instead of a partial da, so the
+// gradients it feeds are visibly poisoned, never silently wrong.  (Round 3 ran the completion in
+// the grid's last workgroup alone: 6.0 ms per launch at cfg2 against 52 us paired.)
 #pragma once
 
 #include <type_traits>
@@ -45,13 +52,17 @@
 
 namespace cgr {
 
-// completers of the unpaired form: half the grid, at most half the CUs (the rest of the grid
-// always has CUs to run on while they wait)
+// completers of the unpaired form: half the grid, at most 16 -- half of one XCD's 32 CUs, so the
+// spinning completers can never occupy every CU an undispatched workgroup could be placed on
 __host__ __device__ inline int unpaired_completers(int grid) {
   const int k = grid / 2;
-  return k < 1 ? 1 : (k > 128 ? 128 : k);
+  return k < 1 ? 1 : (k > 16 ? 16 : k);
 }
-constexpr int kUnpairedSpinLimit = 1 << 22;  // ~0.3 s of s_sleep polling, then status bit 16
+constexpr int kUnpairedSpinLimit = 1 << 22;  // ~0.3 s of s_sleep polling, then reported (above)
+
+// words of the host-visible error block (pinned host memory mapped into the device, one block per
+// device: streams.hip); plain system-scope stores of 1, never read-modify-write across the bus
+enum : int { kDevErrUnpairedTimeout = 0, kDevErrUnpairedSeen = 1, kDevErrWords = 16 };
 
 template <bool EDGE_INIT>
 struct EpLayerBwdSeg {
@@ -66,9 +77,12 @@ struct EpLayerBwdSeg {
   float* dag;          // [nodes, Hp] crossing-segment partial sums of da (zero on entry)
   float* dag_next;     // the next layer's (or null): completed segments' entries zeroed
   float* part;         // [tiles, 2, BN] partials of segments over >= 3 row tiles (slot_of)
-  int* cnt;            // [nodes * tiles_n + 2] tickets (zero on entry, left zero)
+  int* cnt;            // [nodes * tiles_n] segment tickets (zero on entry, left zero)
   const int* status;   // graph prep's status word
   int M, N, nodes, tiles_n;
+  int* gcnt;           // unpaired form: this launch's grid ticket counter (zero on entry)
+  int* dev_err;        // host-visible error words (kDevErr*), or null
+  int spin_limit;      // unpaired completers' wait bound (< 0: report at once; debug knob)
 
   struct Ctx {};
   __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
@@ -184,9 +198,8 @@ struct EpLayerBwdSeg {
             any = any || done;
           }
         } else {
-          int* gc = cnt + (int64_t)nodes * tiles_n;
           const int G = (int)gridDim.x, K = unpaired_completers(G);
-          const int t = __hip_atomic_fetch_add(gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const int t = __hip_atomic_fetch_add(gcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           any = t >= G - K;
           scratch[14] = any ? t - (G - K) : -1;  // completer rank
           scratch[15] = -1;
@@ -243,23 +256,35 @@ struct EpLayerBwdSeg {
         // unpaired completer of rank f0: once every workgroup has drawn its ticket (its raw rows
         // are published), da[v] = sum_{src(e) = v} dm[e] = raw[rev(e)] and every row of v's dst
         // segment, for the nodes v = f0 (mod K), all columns
-        int* gc = cnt + (int64_t)nodes * tiles_n;
         const int G = (int)gridDim.x, K = unpaired_completers(G);
         if (tid == 0) {
           int spins = 0;
-          while (__hip_atomic_load(gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G &&
-                 ++spins < kUnpairedSpinLimit)
-            __builtin_amdgcn_s_sleep(2);
-          if (spins >= kUnpairedSpinLimit) atomicOr(const_cast<int*>(status), 16);
+          bool late = spin_limit < 0;
+          while (!late && __hip_atomic_load(gcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < G) {
+            if (++spins >= spin_limit) late = true;
+            else __builtin_amdgcn_s_sleep(2);
+          }
+          if (late) {
+            atomicOr(const_cast<int*>(status), 16);
+            if (dev_err)
+              __hip_atomic_store(dev_err + kDevErrUnpairedTimeout, 1, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+          if (dev_err && f0 == 0)
+            __hip_atomic_store(dev_err + kDevErrUnpairedSeen, 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+          scratch[13] = late ? 1 : 0;
         }
         __syncthreads();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // loads stay below the wait
+        // a completer that gave up waiting poisons what it writes (NaN), never a partial sum
+        const float poison = scratch[13] ? __builtin_nanf("") : 0.f;
         const int C4all = a.Hp >> 2;
         const int64_t mine = nodes > f0 ? (nodes - f0 + K - 1) / K : 0;
         float ds = 0.f;
         for (int64_t q = tid; q < mine * C4all; q += NT) {
           const int v = f0 + K * (int)(q / C4all), col = 4 * (int)(q % C4all);
-          float4 da = f4zero();
+          float4 da = make_float4(poison, poison, poison, poison);
           for (int j = src_ptr[v], e = src_ptr[v + 1]; j < e; ++j)
             da = f4add(da, sc1_load4(raw + (int64_t)a.rev_s[src_list[j]] * a.Hp + col));
           for (int i = dst_ptr[v], e = dst_ptr[v + 1]; i < e; ++i) {
@@ -269,18 +294,6 @@ struct EpLayerBwdSeg {
           }
         }
         dsig_c[0] = ds;
-        // the last completer to finish resets both grid counters (every completer has passed its
-        // wait by then: it drew its done ticket after it)
-        ep_vm_drain();
-        __syncthreads();
-        if (tid == 0) {
-          const int d = __hip_atomic_fetch_add(gc + 1, 1, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-          if (d == K - 1) {
-            gc[0] = 0;
-            gc[1] = 0;
-          }
-        }
       }
     }
 

@@ -302,6 +302,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   const int seg_cols = lcols.tiles;
   const int seg_tiles = bwd_seg_tiles(d);
   int* cnt = reinterpret_cast<int*>(ws + WL.cnt);
+  const int spin = unpaired_spin_limit();  // CGR_UNPAIRED_SPIN_LIMIT (debug knob), per call
   float* part = reinterpret_cast<float*>(ws + WL.part);
   auto layer_args = [&](int l) {
     uint32_t thresh;
@@ -375,17 +376,18 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       const b3_u4* img = static_cast<const b3_u4*>(fv.b3lb[l]);
       float* dg = dag_of(l);
       float* dgn = l > 0 ? dag_of(l - 1) : nullptr;
+      int* gcnt = cnt + (int64_t)N * seg_cols + l;  // this launch's unpaired grid counter
       if (l > 0)
         HIP_RET(launch_b3nt(al, img, lcols,
                             EpLayerBwdSeg<false>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
                                                  iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
-                                                 seg_cols},
+                                                 seg_cols, gcnt, ss->dev_err, spin},
                             E, H, H, st));
       else
         HIP_RET(launch_b3nt(al, img, lcols,
                             EpLayerBwdSeg<true>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
                                                 iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
-                                                seg_cols},
+                                                seg_cols, gcnt, ss->dev_err, spin},
                             E, H, H, st));
     }
     if (fork_ev) HIP_RET(hipStreamWaitEvent(side, fork_ev, 0));

@@ -528,10 +528,8 @@ __global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
         if (c < a.cnt_tiles) a.cnt[(int64_t)v * a.cnt_tiles + c] = 0;
       }
     }
-    if (t == 0) {  // the grid tickets (unpaired form: arrivals, finished completers)
-      a.cnt[a.cnt_nodes * a.cnt_tiles] = 0;
-      a.cnt[a.cnt_nodes * a.cnt_tiles + 1] = 0;
-    }
+    if (t < CGR_MAX_DEPTH)  // the unpaired form's grid counters, one per fused launch
+      a.cnt[a.cnt_nodes * a.cnt_tiles + t] = 0;
   }
   if (a.dsig_part) block_partial(dsig, a.dsig_part);
 }

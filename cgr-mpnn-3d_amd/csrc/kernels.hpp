@@ -86,7 +86,8 @@ struct LayerBwdArgs {
   int nlayers;
   const float* sig[CGR_MAX_DEPTH];
   // top layer (layer_act_bwd): the entries of dag and of the ticket counters cnt
-  // ([cnt_nodes * cnt_tiles + 2]) the fused layer-backward GEMMs use (nodes whose dst segment
+  // ([cnt_nodes * cnt_tiles + CGR_MAX_DEPTH]: segment tickets, then the unpaired form's grid
+  // counter of each fused launch) the fused layer-backward GEMMs use (nodes whose dst segment
   // crosses a tile_rows row-tile boundary, ep_bwd.hpp) are zeroed (nullable)
   float* dag;
   int* cnt;

@@ -1,10 +1,12 @@
 #include "streams.hpp"
 
 #include <stdlib.h>
+#include <string.h>
 
 #include <mutex>
 #include <string>
 
+#include "ep_bwd.hpp"
 #include "gnn_internal.hpp"
 
 namespace cgr {
@@ -20,6 +22,11 @@ bool single_stream() {
     return v && v[0] == '1';
   }();
   return on;
+}
+
+int unpaired_spin_limit() {
+  const char* v = getenv("CGR_UNPAIRED_SPIN_LIMIT");
+  return v && v[0] ? atoi(v) : kUnpairedSpinLimit;
 }
 
 bool prep_split() {
@@ -85,8 +92,29 @@ SideStreams* side_streams(hipStream_t main) {
     }
   }
   s->next = 0;
+  s->err_host = nullptr;
+  s->dev_err = nullptr;
+  void* h = nullptr;
+  if (hipHostMalloc(&h, sizeof(int) * kDevErrWords, hipHostMallocMapped | hipHostMallocCoherent) ==
+      hipSuccess) {
+    memset(h, 0, sizeof(int) * kDevErrWords);
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, h, 0) == hipSuccess) {
+      s->err_host = static_cast<int*>(h);
+      s->dev_err = static_cast<int*>(dp);
+    } else {
+      (void)hipHostFree(h);
+    }
+  }
+  (void)hipGetLastError();  // a failed pinned allocation only disables the error words
   g_side[dev] = s;
   return s;
+}
+
+SideStreams* side_streams_of(int dev) {
+  if (dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_side[dev];
 }
 
 hipError_t depend(SideStreams* s, hipStream_t from, hipStream_t to) {

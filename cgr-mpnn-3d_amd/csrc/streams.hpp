@@ -18,6 +18,11 @@ struct SideStreams {
   // held by cgr_gnn_forward / _backward for their whole enqueue: two host threads driving one
   // device would otherwise re-record each other's ring events between a record and its wait
   std::mutex mu;
+  // host-visible error words (ep_bwd.hpp kDevErr*): pinned host memory mapped into the device,
+  // written by kernels with plain system-scope stores and read by the host without a sync
+  // (cgr_device_errors); null if the pinned allocation failed
+  int* err_host;
+  int* dev_err;
 };
 
 // CGR_SINGLE_STREAM=1 in the environment: everything on the caller's stream (A/B of the
@@ -29,6 +34,12 @@ bool prep_split();
 
 // returns nullptr and sets the library error if the streams cannot be created
 SideStreams* side_streams(hipStream_t main);
+// the side streams of `device` if they exist (no creation), else nullptr
+SideStreams* side_streams_of(int device);
+
+// CGR_UNPAIRED_SPIN_LIMIT (read per call; tests): the unpaired completers' wait bound in polls
+// (ep_bwd.hpp); negative = report a timeout at once (exercises the error path)
+int unpaired_spin_limit();
 
 // main -> side dependency (side waits for everything enqueued on main so far)
 hipError_t fork_to(SideStreams* s, hipStream_t main, hipStream_t side);

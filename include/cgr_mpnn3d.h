@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CGR_ABI_VERSION 4
+#define CGR_ABI_VERSION 5
 #define CGR_MAX_DEPTH 32
 
 enum cgr_status {
@@ -100,7 +100,8 @@ int64_t cgr_gnn_workspace_bytes(const cgr_gnn_config* cfg, int64_t num_nodes, in
 /* Byte offset of a named arena buffer (introspection for tests/debugging).  "status" is the graph
  * prep's int32 status word: bit 0 an edge id outside [0, num_nodes), bit 1 an unsorted or
  * out-of-range batch vector, bit 2 edges not reverse-paired (src(e ^ 1) != dst(e) for some e;
- * informational: results stay exact, the backward takes its unpaired form).  Names: "status", "rng",
+ * informational: results stay exact, the backward takes its unpaired form), bit 4 (value 16) the
+ * unpaired backward's completion timed out (see cgr_device_errors).  Names: "status", "rng",
  * "perm", "src_s", "dst_s", "rev_s", "src_list", "dst_ptr", "src_ptr", "graph_ptr",
  * "node_graph", "e_s", "P", "h", "a", "pre", "zn", "hn", "g"; `index` selects the layer for
  * "h" / "a" / "pre".  Returns -1 for an unknown or absent buffer. */
@@ -167,6 +168,19 @@ int cgr_gnn_predict(const cgr_gnn_config* cfg, const float* const* params,
                     const cgr_batch* batch, const float* dropout_p, uint64_t seed,
                     uint64_t* rng_counter, int32_t training, const void* images, void* arena,
                     float* y, void* stream);
+
+/* Sticky device-side conditions of `device` (no reference counterpart: the reference's autograd
+ * cannot fail this way), read from pinned host memory the kernels write -- no device sync, so a
+ * caller can poll it at every step.  A condition becomes visible once the kernel that raised it
+ * has run.  Bits (cleared when `clear` != 0):
+ *   CGR_DEVERR_UNPAIRED_TIMEOUT  a completer of the unpaired-edge backward (edges not
+ *       reverse-paired, status bit 2) gave up waiting for the rest of its launch; the gradients
+ *       of that backward are NaN-poisoned, never partial.  An error.
+ *   CGR_DEVERR_UNPAIRED_SEEN  a backward ran the unpaired form (slower; informational).
+ * Returns 0 before the device's first cgr_gnn_forward / _backward. */
+#define CGR_DEVERR_UNPAIRED_SEEN 4
+#define CGR_DEVERR_UNPAIRED_TIMEOUT 16
+int32_t cgr_device_errors(int32_t device, int32_t clear);
 
 /* Segmented sum, the sum-scatter primitive of the path (PyG propagate aggr="add", GNN.py:134;
  * global_add_pool, GNN.py:110) over a CSR: out[s, :] = sum_{j in [seg_ptr[s], seg_ptr[s+1])}
@@ -257,6 +271,13 @@ int64_t cgr_profile_report(char* buf, int64_t len);
  * caller; its first 16 bytes are the record counter) for at most `records` workgroups; NULL stops
  * recording.  The product build returns CGR_ERR_UNSUPPORTED. */
 int cgr_debug_stamps(void* buffer, int64_t records);
+
+/* Process diagnostics (no reference counterpart): on != 0 installs a SIGABRT handler that prints
+ * the aborting thread's id, name and native backtrace to stderr, then passes the signal to the
+ * handler installed before it (e.g. Python's faulthandler) or the default action; 0 restores
+ * that handler.  Used by the multi-process / RCCL tests and the distributed bench, so an abort in
+ * a runtime thread without Python frames still names its origin. */
+int cgr_debug_abort_backtrace(int32_t on);
 
 #ifdef __cplusplus
 }

@@ -2,7 +2,7 @@
 
 The reference trains with `train.py`'s defaults -- depth 3, hidden 300, dropout 0.02
 (train.py:156-166; GNN.py:46-47) -- and its hyper-parameter sweep spans hidden in
-{100, 300, 500, 1000} x depth 2..6 with the learnable skip on or off
+{100, 300, 500, 1000} x depth {2, 3, 4, 5, 6} with the learnable skip on or off
 (hyperparameter_study/sweep_config.json:6-7, expanded at hyperparameter_tuning.py:24-26).  Every
 such width must give the oracle's predictions and gradients (tolerances of test_gpu_parity.py).
 
@@ -52,7 +52,9 @@ def _profiled_classes(m, data):
     return set(rep)
 
 
-SWEEP = [(H, D, skip) for H in (100, 300, 500, 1000) for D in (2, 3, 6) for skip in (False, True)]
+# every sweep depth (sweep_config.json:6: 2..6) x width x learnable skip
+SWEEP = [(H, D, skip) for H in (100, 300, 500, 1000) for D in (2, 3, 4, 5, 6)
+         for skip in (False, True)]
 
 
 @pytest.mark.parametrize("H,D,skip", SWEEP + [(521, 2, False)])

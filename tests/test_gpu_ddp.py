@@ -7,10 +7,14 @@ soon as its event fires.  What is checked here, on one GPU:
     hook-free gradient, eagerly and inside a captured training step -- each event fired after its
     bucket's last write (an early event would let a later write overwrite the doubled values) and
     the buckets cover every parameter once;
-  * a world-1 RCCL process group (backend "nccl", in this process): the real all_reduce(SUM) of
-    every bucket inside a captured step leaves the gradients bitwise equal to the run without the
-    hook, and the process group is then torn down in the order ddp.teardown prescribes (captured
-    graphs first, then the communicator);
+  * a world-1 RCCL process group (backend "nccl"): the real all_reduce(SUM) of every bucket
+    inside a captured step leaves the gradients bitwise equal to the run without the hook, and
+    ddp.teardown then ends it in bench.py's order (graph dropped, sync, hook closed, destroy, and
+    only then a collection) -- with no collection of its own beforehand, after other GPU work has
+    left garbage behind.  It runs in a child process with the native abort backtrace installed
+    (cgr_debug_abort_backtrace), so an abort names its thread and cannot end the suite;
+  * bench.py's distributed path itself (--force-dist 1: RCCL world 1, the collectives captured
+    with the step, ddp.teardown after the JSON line), exit status 0;
   * two real ranks (two processes sharing the one GPU, gloo): each runs the native forward /
     backward on its shard of the cfg2 batch with install_grad_allreduce; the all-reduced gradients
     are bitwise identical on both ranks and equal the whole-batch native gradient (1e-4).
@@ -97,27 +101,69 @@ def _free_port():
     return port
 
 
-def test_world1_rccl_allreduce_inside_captured_step_is_bitwise_identity(cuda_device):
+def _rccl_world1_child():
+    """The world-1 RCCL case in bench.py's order, after other GPU work has left garbage (run as a
+    child process: test_world1_rccl_...)."""
+    from cgr_mpnn_3D._amd import native
     from cgr_mpnn_3D._amd.ddp import teardown
 
-    import gc
+    native.load().cgr_debug_abort_backtrace(1)
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    # earlier work, as the tests before this one leave it: a captured step with a bucket op,
+    # models, arenas and an exception traceback (a reference cycle holding tensors), none of it
+    # collected before the communicator exists
+    m0, d0 = _model(dev)
+    install_grad_allreduce(m0, op=lambda t: t.mul_(2.0))
+    _captured(m0, d0)
+    remove_grad_allreduce(m0)
+    try:
+        keep = _grads(m0, d0)  # noqa: F841
+        raise ValueError("cycle")
+    except ValueError as e:
+        junk = [e]  # noqa: F841  (frame <-> traceback cycle over keep, m0, d0)
+    del m0, d0, keep, junk
 
-    gc.collect()  # what earlier tests left in reference cycles goes before the communicator exists
-    torch.cuda.synchronize()
-    m, data = _model(cuda_device, D=4, H=400, skip=False)
+    m, data = _model(dev, D=4, H=400, skip=False)
     ref = _captured(m, data)
     store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
-    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=cuda_device)
-    try:
-        install_grad_allreduce(m)
-        eager = _grads(m, data)
-        cap = _captured(m, data)  # its graph (with the captured collectives) is gone on return
-        for a, c, r in zip(eager, cap, ref):
-            assert torch.equal(a, r)
-            assert torch.equal(c, r)
-    finally:
-        teardown(m)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=dev)
+    install_grad_allreduce(m)
+    eager = _grads(m, data)
+    cap = _captured(m, data)  # its graph (with the captured collectives) is gone on return
+    ok = all(torch.equal(a, r) and torch.equal(c, r) for a, c, r in zip(eager, cap, ref))
+    teardown(m)
     assert not dist.is_initialized() and m._grad_bucket_hook is None
+    print(f"RCCL_WORLD1_BITWISE={ok}", flush=True)
+
+
+def _run_child(args, timeout=240, env=None):
+    import subprocess
+
+    p = subprocess.run([sys.executable, "-u"] + args, capture_output=True, text=True,
+                       timeout=timeout, env=dict(os.environ, **(env or {})))
+    return p.returncode, p.stdout + p.stderr
+
+
+def test_world1_rccl_allreduce_inside_captured_step_is_bitwise_identity(cuda_device):
+    rc, out = _run_child([os.path.abspath(__file__), "--rccl-world1"])
+    assert rc == 0, out[-4000:]
+    assert "RCCL_WORLD1_BITWISE=True" in out, out[-4000:]
+
+
+def test_bench_distributed_path_rccl_world1_exits_clean(cuda_device):
+    import json
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rc, out = _run_child(
+        [os.path.join(repo, "bench.py"), "--force-dist", "1", "--config", "cfg1", "--steps", "5",
+         "--warmup", "3", "--profile-steps", "0", "--collate-bench", "0", "--infer-bench", "0",
+         "--cpu-baseline", "0"],
+        env={"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_free_port())})
+    assert rc == 0, out[-4000:]
+    line = [ln for ln in out.splitlines() if ln.startswith("{")][-1]
+    j = json.loads(line)
+    assert j["value"] > 0 and j["config"]["parallelism"] == "dp1", j
 
 
 def _two_rank_child(out_dir):
@@ -127,6 +173,9 @@ def _two_rank_child(out_dir):
     from cgr_mpnn_3D._amd.ddp import shard_batch, teardown
     from cgr_mpnn_3D._amd.synth import CONFIGS
 
+    from cgr_mpnn_3D._amd import native
+
+    native.load().cgr_debug_abort_backtrace(1)
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
@@ -184,3 +233,5 @@ def test_two_ranks_on_one_gpu_allreduce_equals_whole_batch(cuda_device, tmp_path
 
 if __name__ == "__main__" and "--two-rank" in sys.argv:
     _two_rank_child(sys.argv[sys.argv.index("--two-rank") + 1])
+if __name__ == "__main__" and "--rccl-world1" in sys.argv:
+    _rccl_world1_child()

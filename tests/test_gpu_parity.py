@@ -6,6 +6,8 @@ Tolerances (north_star: fp32 outputs within 1e-4 relative; index bookkeeping bit
   * integers:     exact equality
 """
 
+import warnings
+
 import numpy as np
 import pytest
 import torch
@@ -13,6 +15,7 @@ import torch.nn.functional as F
 
 from conftest import golden_cases, load_golden
 
+from cgr_mpnn_3D._amd import native
 from cgr_mpnn_3D._amd.debug import ArenaRun
 from cgr_mpnn_3D._amd.synth import TorchBatch, make_batch
 from cgr_mpnn_3D.models.GNN import GNN
@@ -687,6 +690,8 @@ def test_unpaired_edge_order_vs_oracle(act, skip, cuda_device, monkeypatch):
     _oracle_compare(u, 64, 3, act, skip, cuda_device)
     _assert_bitwise_reruns(u, 64, 3, skip, cuda_device)
     # a model warns once (its first forward) when the edge order is not reverse-paired
+    torch.cuda.synchronize()
+    native.raise_device_errors(cuda_device)  # the unpaired backwards above reported themselves
     torch.manual_seed(0)
     for batch, n_warn in ((b, 0), (u, 1)):
         m = GNN(b.x.shape[1], 14, depth=1, hidden_sizes=[16], dropout_ps=[0.0]).to(cuda_device)
@@ -807,3 +812,74 @@ def test_unpaired_edge_order_128_row_tiles_vs_oracle(cuda_device):
     # the completion is split over the grid's last arrivers (which ones varies run to run); every
     # node's sums and every learnable-skip partial sit at places fixed by the data
     _assert_bitwise_reruns(u, 48, 2, True, cuda_device)
+
+
+def _shuffled_pairs(b, seed):
+    from dataclasses import replace
+
+    per = b.edge_index.shape[1] // b.num_graphs
+    rng = np.random.default_rng(seed)
+    order = np.concatenate([g * per + rng.permutation(per) for g in range(b.num_graphs)])
+    return replace(b, edge_index=np.ascontiguousarray(b.edge_index[:, order]),
+                   edge_attr=np.ascontiguousarray(b.edge_attr[order]))
+
+
+def test_unpaired_edge_order_multi_wave_grid_vs_oracle(cuda_device):
+    # more workgroups than CUs (>= 282 row tiles of 128 rows): the unpaired form's 16 completers
+    # wait while later workgroups are still being dispatched (the case a CU-sized
+    # completer set could deadlock); results vs the oracle, and no completer reported a timeout
+    u = _shuffled_pairs(make_batch(600, n_atoms=30, n_bonds=30, n_mace=16, seed=31), seed=7)
+    assert u.edge_index.shape[1] >= 282 * 128
+    assert _pair_status(u, cuda_device) == 4
+    torch.cuda.synchronize()
+    native.raise_device_errors(cuda_device)
+    _oracle_compare(u, 64, 2, "relu", True, cuda_device)
+    torch.cuda.synchronize()
+    bits = native.raise_device_errors(cuda_device)  # raises on a timeout
+    assert bits & native.DEVERR_UNPAIRED_SEEN
+
+
+def test_unpaired_timeout_raises_and_poisons(cuda_device, monkeypatch):
+    # CGR_UNPAIRED_SPIN_LIMIT < 0 makes every unpaired completer report a timeout at once (the
+    # error path of ep_bwd.hpp): the gradients of that backward are NaN, never partial, and the
+    # model's next native call raises; after that the error is cleared
+    u = _shuffled_pairs(make_batch(8, n_atoms=30, n_bonds=30, n_mace=16, seed=28), seed=5)
+    torch.manual_seed(0)
+    m = GNN(u.x.shape[1], 14, depth=2, hidden_sizes=[32] * 2, dropout_ps=[0.0] * 2,
+            use_learnable_skip=True).to(cuda_device).train()
+    data = u.to_torch(cuda_device)
+    torch.cuda.synchronize()
+    native.raise_device_errors(cuda_device)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)
+        m(data)  # first forward: the sync pairing check (warns), outside the timed-out backward
+        monkeypatch.setenv("CGR_UNPAIRED_SPIN_LIMIT", "-1")
+        torch.nn.MSELoss(reduction="sum")(m(data), data.y).backward()
+        torch.cuda.synchronize()
+        monkeypatch.delenv("CGR_UNPAIRED_SPIN_LIMIT")
+        assert torch.isnan(m.edge_init.weight.grad).any()
+        with pytest.raises(RuntimeError, match="timed out"):
+            m(data)
+        m.zero_grad(set_to_none=True)
+        torch.nn.MSELoss(reduction="sum")(m(data), data.y).backward()
+        torch.cuda.synchronize()
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+    native.raise_device_errors(cuda_device)
+
+
+def test_unpaired_batch_after_paired_ones_warns_without_a_sync(cuda_device):
+    # the first forward's pairing check sees a paired batch; a later unpaired batch is reported by
+    # its backward through the device error words, and the next forward warns once
+    b = make_batch(8, n_atoms=30, n_bonds=30, n_mace=16, seed=28)
+    u = _shuffled_pairs(b, seed=5)
+    torch.manual_seed(0)
+    m = GNN(b.x.shape[1], 14, depth=2, hidden_sizes=[32] * 2, dropout_ps=[0.0] * 2).to(
+        cuda_device).train()
+    torch.cuda.synchronize()
+    native.raise_device_errors(cuda_device)
+    with _WarnCount() as wc:
+        for batch in (b, u, b, b):
+            d = batch.to_torch(cuda_device)
+            torch.nn.MSELoss(reduction="sum")(m(d), d.y).backward()
+            torch.cuda.synchronize()
+    assert wc.count == 1

@@ -29,8 +29,10 @@ def say(*a):
 def main():
     from test_gpu_ddp import _captured, _grads, _model
 
-    from cgr_mpnn_3D._amd.ddp import install_grad_allreduce, remove_grad_allreduce
+    from cgr_mpnn_3D._amd import native
+    from cgr_mpnn_3D._amd.ddp import install_grad_allreduce, teardown
 
+    native.load().cgr_debug_abort_backtrace(1)  # an abort names its thread and native stack
     dev = torch.device("cuda:0")
     m, data = _model(dev, D=4, H=400, skip=False)
     ref = _captured(m, data)
@@ -73,10 +75,8 @@ def main():
     gc.garbage.clear()
     gc.collect()
     torch.cuda.synchronize()
-    say("all freed; closing the hook")
-    remove_grad_allreduce(m)
-    say("hook closed; destroying the process group")
-    dist.destroy_process_group()
+    say("all freed; ddp.teardown (hook closed, process group destroyed, then collected)")
+    teardown(m)
     say("destroyed")
 
 
