@@ -228,7 +228,10 @@ def backward(params: dict, cache: dict, dy: np.ndarray) -> dict:
         grads[f"convs.{l}.lin.weight"] = dz.T @ cache["ms"][l]
         grads[f"convs.{l}.lin.bias"] = dz.sum(0)
         if cache["learnable_skip"]:
-            grads[f"skip_weights.{l}"] = np.asarray((dz * cache["hs"][0]).sum())
+            t = dz * cache["hs"][0]
+            grads[f"skip_weights.{l}"] = np.asarray(t.sum())
+            # sum |terms| of that scalar reduction: its conditioning (tests scale the bar by it)
+            cache.setdefault("skip_abs", {})[f"skip_weights.{l}"] = float(np.abs(t).sum())
         dh0 += cache["sig"][l] * dz
         dm = dz @ Wl  # [E, H]
         da = _scatter_sum(dm, src, N)  # m = a[src] - h[rev]  ->  da = scatter_src(dm)
@@ -241,11 +244,14 @@ def backward(params: dict, cache: dict, dy: np.ndarray) -> dict:
 
 
 def loss_and_grads(params, x, edge_index, edge_attr, batch, y_true, depth, act="relu",
-                   learnable_skip=False, num_graphs=None, relu_masks=None):
-    """MSELoss(reduction='sum') (train.py:120) forward + backward: (loss, y_hat, grads)."""
+                   learnable_skip=False, num_graphs=None, relu_masks=None, cache_out=None):
+    """MSELoss(reduction='sum') (train.py:120) forward + backward: (loss, y_hat, grads).
+    `cache_out` (a dict, optional) receives the forward / backward cache (incl. "skip_abs")."""
     y, cache = forward(params, x, edge_index, edge_attr, batch, depth, act, learnable_skip,
                        num_graphs, relu_masks=relu_masks)
     r = y - np.asarray(y_true, np.float64)
     loss = float((r * r).sum())
     grads = backward(params, cache, 2.0 * r)
+    if cache_out is not None:
+        cache_out.update(cache)
     return loss, y, grads
