@@ -103,12 +103,14 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("pool_head_fwd", 1, 2.0 * N * H, f4 * (N * H + B * H + H + B) + i4 * (B + 1))
     # backward
     add("head_bwd", 1, 2.0 * B * H, f4 * (B + B * H + 2 * H))  # dwf = dy^T g, dbf
-    # dzn = dy[graph] wf * act'(zn): hn (ReLU mask) read, dzn written (+ the da zeroing it carries)
+    # dzn = dy[graph] wf * act'(zn): hn (ReLU mask) read, dzn's e-image written (2 bf16 pieces,
+    # the readout TN's operand; fp32 dzn itself is not stored)
     add("readout_act_bwd", 1, 0.0, f4 * (B + H + 2 * N * H) + i4 * N)
     add("gemm_tn_wgrad_readout", 1, 2.0 * N * H * (F + H),
         f4 * (N * H + N * F + N * H + H * (F + H) + H))
     add("gemm_nt_readout_bwd", 1, 2.0 * N * H * H, f4 * (N * H + H * H + N * H))
-    add("layer_act_bwd", 1, 0.0, f4 * (N * H + 2 * E * H) + i4 * E)  # top layer: dh = ds[dst]
+    # top layer: dh = ds[dst]; dpre written in fp32 and as the layer TN's e-image (2 bf16 pieces)
+    add("layer_act_bwd", 1, 0.0, f4 * (N * H + 3 * E * H) + i4 * E)
     add("gemm_tn_wgrad_layer", D, 2.0 * E * H * H,
         f4 * (E * H + N * H + E * H + H * H + H) + 2 * i4 * E)
     # dm = dpre_l W_l with da = segsum_src(dm) and the layer below's activation backward in its
@@ -119,9 +121,10 @@ def algorithmic_work(N, E, B, F, Fe, H, D, relu=True):
     add("segsum_src_bwd", 1, E * H, seg_dst + i4 * E)  # Gs = segsum_src(dpre0) for dW0[:, :F]
     add("gemm_tn_wgrad_edge", 1, 2.0 * E * H * Fe, f4 * (E * H + E * Fe + H * Fe + H))
     add("gemm_tn_wgrad_node", 1, 2.0 * N * H * F, f4 * (N * H + N * F + H * F))
-    # e-images of the weight gradients' shared operand (dpre_l, dzn): fp32 in, 2 bf16 out (Gs's
-    # is written by segsum_src_bwd itself)
-    add("eimage", D + 1, 0.0, f4 * (D * E * H + N * H) * 2 / (D + 1))
+    # e-images of the weight gradients' shared operand dpre_l for the layers below the top: fp32
+    # in, 2 bf16 out (dzn's and the top layer's dpre's are written by their producers, Gs's by
+    # segsum_src_bwd)
+    add("eimage", max(D - 1, 1), 0.0, f4 * E * H * 2)
     # split-bf16 weight images, once per step: fp32 weights in, three bf16 pieces out
     nw = 2 * H * F + (2 + 2 * D) * H * H
     add("weight_pack", 1, 0.0, (f4 + 3 * 2.0) * nw)

@@ -32,8 +32,9 @@ __device__ __forceinline__ RowOps layer_row_loads(const LayerBwdArgs& a, int64_t
 // A >= 0: the activation as a compile-time constant (one straight-line path per activation, no
 // per-element branch tree); A < 0: a.act at run time
 template <int A = -1>
-__device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
-                                                uint64_t key, float& dsig, const RowOps& r) {
+__device__ __forceinline__ float4 layer_row_apply(const LayerBwdArgs& a, int64_t i, int n,
+                                                  float4 dh, uint64_t key, float& dsig,
+                                                  const RowOps& r) {
   const int act = A < 0 ? a.act : A;
   const int64_t o = i * a.Hp + n;
   float d[4] = {dh.x, dh.y, dh.z, dh.w};
@@ -60,6 +61,7 @@ __device__ __forceinline__ void layer_row_apply(const LayerBwdArgs& a, int64_t i
     for (int k = 0; k < 4; ++k)
       if (n + k < a.H) dsig += d[k] * hz[k];
   }
+  return dp;
 }
 
 __device__ __forceinline__ RowOps edge_row_loads(const LayerBwdArgs& a, int64_t i, int n) {
@@ -110,7 +112,7 @@ template <bool EDGE_INIT, int A = -1>
 __device__ __forceinline__ void bwd_row_apply(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
                                               uint64_t key, float& dsig, const RowOps& r) {
   if constexpr (EDGE_INIT) edge_row_apply<A>(a, i, n, dh, r);
-  else layer_row_apply<A>(a, i, n, dh, key, dsig, r);
+  else (void)layer_row_apply<A>(a, i, n, dh, key, dsig, r);
 }
 
 }  // namespace cgr

@@ -267,6 +267,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   W.Gs = b.take(4 * N * Hp);
   W.img_side = b.take(b3_eimg_bytes(std::max(d.E, d.N), d.H));
   W.img_main = b.take(b3_eimg_bytes(d.N, d.H));
+  W.img_top = b.take(b3_eimg_bytes(d.E, d.H));
   // split-K slabs: every plan a call site may pick for its shape (gnn_bwd.hip), the largest wins.
   // The side-stream weight gradients (readout, layers, edge features) run one after another and
   // share `slab`; the node weight gradient runs beside them on the caller's stream: `slab2`.

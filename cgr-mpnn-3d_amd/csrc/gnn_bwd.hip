@@ -143,6 +143,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   float* dsig_part = reinterpret_cast<float*>(ws + WL.dsig_part);
   void* img_side = ws + WL.img_side;
   void* img_main = ws + WL.img_main;
+  void* img_top = ws + WL.img_top;
   // partial sums of tile-crossing segments, accumulated by layer l's fused backward GEMM: two
   // buffers, alternating by layer (a segment's completer zeroes its entries of the next one)
   auto dag_of = [&](int l) {
@@ -206,17 +207,24 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // side: dwf, dbf; dzn; dW_n = dzn^T [x | s], db_n (forked before the main stream's readout NT:
   // deferring it behind a layer, or enqueuing the NT first, A/B -4..-14 %).  dzn is materialised
   // for the weight gradient only: the main stream's NT forms it inside the GEMM (LdActGrad).
-  {
-    HIP_RET(fork_to(ss, st, side));
+  auto side_readout = [&]() -> int {
     {  // dwf = dy^T g, dbf: off the main chain (step A/B +0.8 %)
       ProfScope _p("head_bwd", side);
       HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
                        grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], side));
     }
+    // the split-bf16 e-image TN takes dzn as the e-image the dzn kernel writes (dzn itself is
+    // then never stored); the fp32 families read dzn
+    const bool ro_b3 =
+        fv.xp ? (b3tni_ok(LdConcat<4>{fv.xp, d.Fp, fv.a[D], Hp, d.Fp}, H, N) &&
+                 ((uintptr_t)fv.xp & 15) == 0)
+              : (F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 &&
+                 b3tni_ok(LdConcat<4>{b->x, F, fv.a[D], Hp, F}, H, N));
     {
       ProfScope _p("readout_act_bwd", side);
       HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
-                              Hp, d.act, dzn, side));
+                              Hp, d.act, ro_b3 ? nullptr : dzn, ro_b3 ? img_side : nullptr,
+                              side));
     }
     TnPlan p;
     float* sl = slabs[sb];
@@ -229,9 +237,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       LdPlain<4> al{dzn, Hp};
       LdConcat<4> bl{fv.xp, Fp, fv.a[D], Hp, Fp};
       const RedJob mine = make_red_job(TnPlan{}, sl, bsl, H, Fp + H, gW, F + H, 0, gb, F, Fp - F);
-      if (b3tni_ok(bl, H, N) && ((uintptr_t)fv.xp & 15) == 0) {
-        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl, H, Fp + H, N, sl, bsl,
-                           true, &p, side, kB3TnReadoutTarget, pend.job));
+      if (ro_b3) {
+        HIP_RET(b3tni_run("gemm_tn_wgrad_readout", img_side, bl, H, Fp + H, N, sl, bsl, true, &p,
+                          side, kB3TnReadoutTarget, pend.job));
         RedJob j = mine;
         j.splits = p.splits;
         if (const int rc = fold(j, 0)) return rc;
@@ -251,9 +259,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     } else {
       const LdConcat<4> bl4{b->x, F, fv.a[D], Hp, F};
       const RedJob mine = make_red_job(TnPlan{}, sl, bsl, H, F + H, gW, F + H, 0, gb);
-      if (F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 && b3tni_ok(bl4, H, N)) {
-        HIP_RET(b3tni_gemm("gemm_tn_wgrad_readout", dzn, Hp, img_side, bl4, H, F + H, N, sl, bsl,
-                           true, &p, side, kB3TnReadoutTarget, pend.job));
+      if (ro_b3) {
+        HIP_RET(b3tni_run("gemm_tn_wgrad_readout", img_side, bl4, H, F + H, N, sl, bsl, true, &p,
+                          side, kB3TnReadoutTarget, pend.job));
         RedJob j = mine;
         j.splits = p.splits;
         if (const int rc = fold(j, 0)) return rc;
@@ -276,10 +284,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         if (const int rc = unfolded(j, 0)) return rc;
       }
     }
-  }
+    return 0;
+  };
   // main: ds = dzn W_n[:, F:] = diag(dy[graph]) act'(zn) (diag(wf) W_n[:, F:]) -- the row factor in
   // the epilogue, the column factor in the weight image (gnn_fwd.hip), act' in the A loader
-  {
+  auto readout_nt = [&]() -> int {
     ProfScope _p("gemm_nt_readout_bwd", st);
     const float* m = d.act == ACT_RELU ? fv.hn : fv.zn;
     const b3_u4* img = static_cast<const b3_u4*>(fv.b3rob);
@@ -292,6 +301,23 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       HIP_RET(launch_b3nt(LdActGradT<ACT_SILU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
     else
       HIP_RET(launch_b3nt(LdActGradT<ACT_GELU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
+    return 0;
+  };
+  // capture order: with CGR_RO_MAIN_FIRST=1 (read per call) the fork point is recorded, the main
+  // stream's NT enqueued and the side work after it -- the same dependencies, but in a captured
+  // graph the runtime then keeps the NT on the forward's hardware queue and gives the side
+  // chain the other one (r05 trace: enqueued second, the NT started 11.6 us after the loss
+  // backward, a cross-queue edge on the critical chain)
+  if (ro_main_first() && side != st) {
+    hipEvent_t ro_ev = nullptr;
+    HIP_RET(record_point(ss, st, &ro_ev));
+    if (const int rc = readout_nt()) return rc;
+    HIP_RET(hipStreamWaitEvent(side, ro_ev, 0));
+    if (const int rc = side_readout()) return rc;
+  } else {
+    if (side != st) HIP_RET(fork_to(ss, st, side));
+    if (const int rc = side_readout()) return rc;
+    if (const int rc = readout_nt()) return rc;
   }
 
   // learnable-skip partial-sum slots per layer (bwd_dsig_slots)
@@ -329,6 +355,10 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.dsig_part = d.learnable_skip ? dsig_part + (int64_t)l * nb : nullptr;
     return la;
   };
+  // the top layer's weight gradient on the split-bf16 e-image TN takes dpre_{D-1}'s e-image from
+  // the activation kernel that writes dpre_{D-1} (no e-image pass over it)
+  const bool top_b3 =
+      D > 0 && b3tni_ok(LdGatherDiff<false>{fv.a[D - 1], fv.h[D - 1], iv.src_s, iv.rev_s, Hp}, H, E);
   if (D > 0) {  // top layer: dh_D = ds[dst]
     ProfScope _p("layer_act_bwd", st);
     LayerBwdArgs la = layer_args(D - 1);
@@ -337,7 +367,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     la.cnt_nodes = N;
     la.cnt_tiles = seg_cols;
     la.tile_rows = seg_rows;
-    HIP_RET(layer_act_bwd(la, nb, st));
+    HIP_RET(layer_act_bwd(la, nb, top_b3 ? img_top : nullptr, st));
   }
   auto edge_args = [&]() {
     LayerBwdArgs le{};
@@ -401,7 +431,12 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       RedJob mine = make_red_job(TnPlan{}, sl, bsl, H, H, grads[CGR_PARAM_CONV_W(l)], H, 0,
                                  grads[CGR_PARAM_CONV_B(l)]);
       const int tf = tnr_layer_frags(H);
-      if (b3tni_ok(bl, H, E)) {
+      if (l == D - 1 && top_b3) {
+        HIP_RET(b3tni_run("gemm_tn_wgrad_layer", img_top, bl, H, H, E, sl, bsl, true, &p, side,
+                          kB3TnTarget, pend.job));
+        mine.splits = p.splits;
+        if (const int rc = fold(mine, D - l)) return rc;
+      } else if (b3tni_ok(bl, H, E)) {
         HIP_RET(b3tni_gemm("gemm_tn_wgrad_layer", dp, Hp, img_side, bl, H, H, E, sl, bsl, true,
                            &p, side, kB3TnTarget, pend.job));
         mine.splits = p.splits;

@@ -117,8 +117,9 @@ struct WorkspaceLayout {
       bslab_elems;
   size_t slab_b, bslab_b;  // the side stream's second slab pair (reductions folded into TNs)
   // split-bf16 e-images (gemm_b3.hpp B3EImg) of the weight gradients' shared operand: dpre_l and
-  // dzn on the side stream (one at a time), Gs on the caller's stream
-  size_t img_side, img_main;
+  // dzn on the side stream (one at a time), Gs on the caller's stream; the top layer's dpre,
+  // written by its activation kernel on the caller's stream (img_top)
+  size_t img_side, img_main, img_top;
   // 2 x [N, Hp] partial da sums of the dst segments that cross a row tile of the fused
   // layer-backward GEMM (ep_bwd.hpp), alternating by layer
   size_t dag;

@@ -412,135 +412,13 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_readout_bwd(const float* __restrict__ dy,
-                                                     const float* __restrict__ wf,
-                                                     const int* __restrict__ node_graph,
-                                                     const float* __restrict__ hn,
-                                                     const float* __restrict__ zn, int64_t N,
-                                                     int H, int Hp, int act,
-                                                     float* __restrict__ dzn) {
-  const int C4 = Hp >> 2;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= N * C4) return;
-  const int64_t v = t / C4;
-  const int c = (int)(t - v * C4);
-  const int n = 4 * c;
-  const int64_t o = v * Hp + n;
-  const float d = dy[node_graph[v]];
-  float4 r;
-  r.x = d * wf[min(n, H - 1)];
-  r.y = d * wf[min(n + 1, H - 1)];
-  r.z = d * wf[min(n + 2, H - 1)];
-  r.w = d * wf[min(n + 3, H - 1)];
-  if (act == ACT_RELU) {
-    const float4 h = *reinterpret_cast<const float4*>(hn + o);
-    r.x = h.x > 0.f ? r.x : 0.f;
-    r.y = h.y > 0.f ? r.y : 0.f;
-    r.z = h.z > 0.f ? r.z : 0.f;
-    r.w = h.w > 0.f ? r.w : 0.f;
-  } else {
-    const float4 z = *reinterpret_cast<const float4*>(zn + o);
-    r.x *= act_grad(z.x, act);
-    r.y *= act_grad(z.y, act);
-    r.z *= act_grad(z.z, act);
-    r.w *= act_grad(z.w, act);
-  }
-  *reinterpret_cast<float4*>(dzn + o) = r;
-}
-
-hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
-                           const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
-                           float* dzn, hipStream_t st) {
-  const int64_t tot = N > 0 ? N * (Hp / 4) : 0;
-  if (tot <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_readout_bwd, dim3(cdiv(tot, 256)), dim3(256), 0, st, dy, wf, node_graph,
-                     hn, zn, N, H, Hp, act, dzn);
-  return hipGetLastError();
-}
+// (k_readout_bwd_img, the dzn kernel, lives in b3_pack.hip: it writes the e-image too)
 
 // ------------------------------------------------------------------------------------------
 // backward: D-MPNN layer activation / skip / dropout (GNN.py:94-102 reversed)
 // ------------------------------------------------------------------------------------------
-int layer_act_bwd_blocks(int64_t E, int Hp) { return (int)cdiv(E * (Hp / 4), 256); }
-
-// one float4 of one edge row of the layer backward, given dh = dL/dh_{l+1}[i, n..n+3]:
-// dpre = dh * keep/(1-p) * act'(pre) ; dsig += dpre . h0  (dh0 = sum_l sigma_l dpre_l is formed
-// by the edge-init backward from the per-layer dpre buffers)
-__device__ __forceinline__ void layer_bwd_row(const LayerBwdArgs& a, int64_t i, int n, float4 dh,
-                                              uint64_t key, float& dsig) {
-  const int64_t o = i * a.Hp + n;
-  float d[4] = {dh.x, dh.y, dh.z, dh.w};
-  if (a.act == ACT_RELU) {  // h_{l+1} > 0 <=> relu active and kept by dropout
-    const float4 hv = *reinterpret_cast<const float4*>(a.hnext + o);
-    const float hh[4] = {hv.x, hv.y, hv.z, hv.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) d[k] = hh[k] > 0.f ? d[k] * a.scale : 0.f;
-  } else {
-    const float4 zv = *reinterpret_cast<const float4*>(a.pre + o);
-    const float zz[4] = {zv.x, zv.y, zv.z, zv.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float m = a.scale;
-      if (a.thresh && n + k < a.H)
-        m = drop_keep(key, (uint32_t)a.layer, (uint64_t)i * a.H + n + k, a.thresh) ? a.scale
-                                                                                      : 0.f;
-      d[k] = d[k] * m * act_grad(zz[k], a.act);
-    }
-  }
-  const float4 dp = make_float4(d[0], d[1], d[2], d[3]);
-  *reinterpret_cast<float4*>(a.dpre + o) = dp;
-  if (a.dsig_part) {
-    const float4 h0 = *reinterpret_cast<const float4*>(a.h0 + o);
-    const float hz[4] = {h0.x, h0.y, h0.z, h0.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (n + k < a.H) dsig += d[k] * hz[k];
-  }
-}
-
-__device__ __forceinline__ void block_partial(float v, float* dst) {
-  __shared__ float red[4];
-  v = wave_sum(v);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  if (threadIdx.x == 0) dst[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
-}
-
-__global__ __launch_bounds__(256) void k_layer_bwd(LayerBwdArgs a) {
-  const int C4 = a.Hp >> 2;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  float dsig = 0.f;
-  if (t < a.E * C4) {
-    const int64_t i = t / C4;
-    const int n = 4 * (int)(t - i * C4);
-    // top layer: dh_D[i] = ds[dst(i)] (lower layers: the fused dm GEMM, ep_bwd.hpp)
-    const float4 dh = *reinterpret_cast<const float4*>(a.ds + (int64_t)a.dst_s[i] * a.Hp + n);
-    layer_bwd_row(a, i, n, dh, a.thresh ? *a.seed : 0, dsig);
-  }
-  if (a.dag) {  // zero what the fused layer-backward GEMMs accumulate (see EpLayerBwdSeg)
-    const int64_t nb = cdiv(a.E, a.tile_rows) - 1;  // interior row-tile boundaries
-    if (t < nb * C4) {
-      const int64_t m = (t / C4 + 1) * a.tile_rows;
-      const int c = (int)(t % C4);
-      const int v = a.dst_s[m];
-      if (a.dst_s[m - 1] == v) {
-        *reinterpret_cast<float4*>(a.dag + (int64_t)v * a.Hp + 4 * c) = f4zero();
-        if (c < a.cnt_tiles) a.cnt[(int64_t)v * a.cnt_tiles + c] = 0;
-      }
-    }
-    if (t < CGR_MAX_DEPTH)  // the unpaired form's grid counters, one per fused launch
-      a.cnt[a.cnt_nodes * a.cnt_tiles + t] = 0;
-  }
-  if (a.dsig_part) block_partial(dsig, a.dsig_part);
-}
-
-hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st) {
-  const int need = layer_act_bwd_blocks(a.E, a.Hp);
-  const int nb = nblocks > need ? nblocks : need;  // extra blocks write zero partials
-  if (need <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_layer_bwd, dim3(nb), dim3(256), 0, st, a);
-  return hipGetLastError();
-}
+// (the top layer's activation backward, k_layer_bwd_img, lives in b3_pack.hip: it writes the
+// weight gradient's e-image of dpre as well)
 
 // ------------------------------------------------------------------------------------------
 // x rows padded to a multiple of 4 floats (F = 846 -> 848): every GEMM that reads x then issues

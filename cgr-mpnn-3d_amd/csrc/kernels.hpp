@@ -54,9 +54,10 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
                     float* dg, float* dwf, float* dbf, hipStream_t st);
 
 // dzn[v] = dy[graph(v)] * wf * act'(zn[v])   (ReLU: hn > 0)
+// dzn (may be null: not materialised) and/or its e-image `img` (gemm_b3.hpp B3EImg; null: none)
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
-                           float* dzn, hipStream_t st);
+                           float* dzn, void* img, hipStream_t st);
 
 struct LayerBwdArgs {
   // dh_{l+1}: top layer (l == D-1, layer_act_bwd): ds[dst_s[i]]; below (the fused dm GEMM,
@@ -95,7 +96,8 @@ struct LayerBwdArgs {
   int tile_rows, cnt_tiles;
 };
 // nblocks: grid size if larger than needed (the learnable-skip partial slots to fill), else 0
-hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, hipStream_t st);
+// img (nullable): the e-image of dpre for the layer's weight-gradient TN, written beside it
+hipError_t layer_act_bwd(const LayerBwdArgs& a, int nblocks, void* img, hipStream_t st);
 int layer_act_bwd_blocks(int64_t E, int Hp);
 // dst[n, col_off + k] = sum_s slab[s, n, k] ; bias_dst[n] = sum_s bslab[s, n]
 // gap_len > 0: slab columns [gap_at, gap_at + gap_len) are padding and skipped; later columns

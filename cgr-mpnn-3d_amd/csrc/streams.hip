@@ -24,6 +24,11 @@ bool single_stream() {
   return on;
 }
 
+bool ro_main_first() {
+  const char* v = getenv("CGR_RO_MAIN_FIRST");
+  return v && v[0] == '1';
+}
+
 int unpaired_spin_limit() {
   const char* v = getenv("CGR_UNPAIRED_SPIN_LIMIT");
   return v && v[0] ? atoi(v) : kUnpairedSpinLimit;
