@@ -183,19 +183,23 @@ def roofline_entry(name, work, launches, ms_total, traffic):
     return out
 
 
-def scatter_add_roofline(edge_index, N, H, dev, reps=50):
+def scatter_add_roofline(edge_index, N, H, dev, reps=50, cold_copies=24, which=None):
     """The path's scatter-add (PyG propagate aggr='add', GNN.py:134) as the native forward runs
     it -- cgr_segment_sum over the dst-sorted edge rows [E, H] into [N, H] -- and its backward
     twin (rows gathered through the src permutation), each timed as `reps` back-to-back launches
     between two HIP events on the launch stream (a single ~8 us launch between events also
-    times the event/dispatch gap).  Inputs are HBM-resident, sized like the bench batch."""
+    times the event/dispatch gap).  Inputs are HBM-resident, sized like the bench batch.
+
+    Two cache states: "warm" re-reads one input, which (24.6 MB at cfg2) stays in the 256 MB
+    Infinity Cache between launches, so it measures the cache more than HBM; "cold" rotates over
+    `cold_copies` distinct inputs and outputs (> 256 MB per rotation: 24 x 36.9 MB = 886 MB at
+    cfg2), so every launch streams from HBM.  `which`: only these (name, state) pairs (the PMC
+    tool, tools/scatter_pmc.py)."""
     from cgr_mpnn_3D._amd import native
 
     lib = native.load()
     E = edge_index.shape[1]
     src, dst = edge_index[0], edge_index[1]
-    vals = torch.randn(E, H, device=dev)
-    out = torch.empty(N, H, device=dev)
 
     def csr(keys):
         deg = torch.bincount(keys, minlength=N)
@@ -208,26 +212,45 @@ def scatter_add_roofline(edge_index, N, H, dev, reps=50):
     perm_src = torch.argsort(src, stable=True).to(torch.int32)
     stream = torch.cuda.current_stream(dev)
     res = {}
-    for name, idx, ptr in (("segsum_dst_fwd", None, ptr_dst), ("segsum_src_bwd", perm_src, ptr_src)):
-        def launch():
-            native.check(lib.cgr_segment_sum(native.ptr(vals), H, native.ptr(idx), native.ptr(ptr),
-                                             N, H, native.ptr(out), H, stream.cuda_stream))
-        for _ in range(5):
-            launch()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        for _ in range(reps):
-            launch()
-        e1.record(stream)
-        e1.synchronize()
-        us = e0.elapsed_time(e1) * 1e3 / reps
-        nbytes = 4.0 * (E * H + N * H) + 4.0 * (N + 1) + (4.0 * E if idx is not None else 0.0)
-        res[name] = {"kernel": name, "bound": "hbm", "achieved": round(nbytes / us / 1e3, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
-                     "algorithmic_bytes_per_launch": nbytes, "avg_launch_us": round(us, 3),
-                     "timing": f"{reps} back-to-back cgr_segment_sum launches between HIP events "
-                               f"on the launch stream, E={E} rows x H={H} -> N={N}"}
+    for state in ("warm", "cold"):
+        copies = 1 if state == "warm" else max(1, cold_copies)
+        if which is not None and not any(w[1] == state for w in which):
+            continue
+        vals = [torch.randn(E, H, device=dev) for _ in range(copies)]
+        outs = [torch.empty(N, H, device=dev) for _ in range(copies)]
+        for name, idx, ptr in (("segsum_dst_fwd", None, ptr_dst),
+                               ("segsum_src_bwd", perm_src, ptr_src)):
+            if which is not None and (name, state) not in which:
+                continue
+
+            def launch(i):
+                native.check(lib.cgr_segment_sum(native.ptr(vals[i % copies]), H,
+                                                 native.ptr(idx), native.ptr(ptr), N, H,
+                                                 native.ptr(outs[i % copies]), H,
+                                                 stream.cuda_stream))
+            for i in range(5):
+                launch(i)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for i in range(reps):
+                launch(5 + i)
+            e1.record(stream)
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            nbytes = 4.0 * (E * H + N * H) + 4.0 * (N + 1) + (4.0 * E if idx is not None else 0.0)
+            res[(name, state)] = {
+                "kernel": name, "bound": "hbm", "achieved": round(nbytes / us / 1e3, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(nbytes / us / 1e3 / HBM_PEAK_GBS, 4),
+                "algorithmic_bytes_per_launch": nbytes, "avg_launch_us": round(us, 3),
+                "cache_state": state,
+                "timing": f"{reps} back-to-back cgr_segment_sum launches between HIP events on the "
+                          f"launch stream, E={E} rows x H={H} -> N={N}"
+                          + (f", rotating over {copies} distinct input/output pairs "
+                             f"({copies * nbytes / 1e6:.0f} MB per rotation > the 256 MB "
+                             f"Infinity Cache)" if copies > 1 else
+                             ", one input re-read (Infinity-Cache resident)")}
+        del vals, outs
     return res
 
 
@@ -564,9 +587,13 @@ def main():
             dom = max(cands, key=lambda k: rep[k][1])
             roof = roofline_entry(dom, work[dom], rep[dom][0], rep[dom][1], hbm(dom))
         sc = scatter_add_roofline(data.edge_index, N, H, dev)
-        roof_scatter = sc["segsum_dst_fwd"]
-        roof_scatter["traffic"] = hbm("segsum_dst_fwd")
-        roof_scatter["backward_gather_twin"] = sc["segsum_src_bwd"]
+        # the headline is the HBM-streaming (cold) form; the cache-resident one is reported beside
+        roof_scatter = sc[("segsum_dst_fwd", "cold")]
+        roof_scatter["traffic"] = hbm("segsum_dst_fwd_cold")
+        roof_scatter["warm_cache"] = dict(sc[("segsum_dst_fwd", "warm")],
+                                          traffic=hbm("segsum_dst_fwd"))
+        roof_scatter["backward_gather_twin"] = dict(sc[("segsum_src_bwd", "cold")],
+                                                    traffic=hbm("segsum_src_twin_cold"))
         # inside the step: the forward's scatter-adds run in the layer GEMM's epilogue (no
         # kernel of their own); the backward's Gs = segsum_src(dpre0) is a standalone one
         if "segsum_src_bwd" in rep:

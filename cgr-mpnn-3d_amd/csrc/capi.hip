@@ -8,7 +8,6 @@
 #include <unordered_map>
 
 #include "dispatch.hpp"
-#include "ep_bwd.hpp"
 #include "gnn_internal.hpp"
 #include "kernels.hpp"
 #include "streams.hpp"

@@ -175,4 +175,11 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// the unpaired form of the fused layer backward (ep_bwd.hpp): its completers' wait bound in polls
+// (~0.3 s of s_sleep polling), after which they report a timeout
+constexpr int kUnpairedSpinLimit = 1 << 22;
+// words of the host-visible error block (pinned host memory mapped into the device, one block per
+// device: streams.hip); plain system-scope stores of 1, never read-modify-write across the bus
+enum : int { kDevErrUnpairedTimeout = 0, kDevErrUnpairedSeen = 1, kDevErrWords = 16 };
+
 }  // namespace cgr

@@ -58,11 +58,7 @@ __host__ __device__ inline int unpaired_completers(int grid) {
   const int k = grid / 2;
   return k < 1 ? 1 : (k > 16 ? 16 : k);
 }
-constexpr int kUnpairedSpinLimit = 1 << 22;  // ~0.3 s of s_sleep polling, then reported (above)
 
-// words of the host-visible error block (pinned host memory mapped into the device, one block per
-// device: streams.hip); plain system-scope stores of 1, never read-modify-write across the bus
-enum : int { kDevErrUnpairedTimeout = 0, kDevErrUnpairedSeen = 1, kDevErrWords = 16 };
 
 template <bool EDGE_INIT>
 struct EpLayerBwdSeg {

@@ -65,8 +65,9 @@ static hipError_t tnr_gemm(const char* name, const SA& sa, const SB& sb, int Nou
   return launch_gemm_tnr<FA, FB>(sa, sb, q, slab, bslab, Nout, Kout, R, want_bias, st);
 }
 
-// split-bf16 TN with the n-side operand A [R, Nout] as an e-image (gemm_b3.hpp): A is split
-// once by b3_eimage into `img`, then every k-tile of the GEMM reads it pre-split
+// split-bf16 TN with the n-side operand A [R, Nout] as an e-image (gemm_b3.hpp): A was split
+// once into `img` (by its producer -- the dzn and top-layer dpre kernels, the Gs segmented sum --
+// or by b3_eimage), then every k-tile of the GEMM reads it pre-split
 // prev: a previous weight gradient's slab reduction folded into this launch (gemm_b3.hpp)
 template <class BL>
 static hipError_t b3tni_run(const char* name, const void* img, const BL& bl, int Nout, int Kout,
@@ -78,19 +79,6 @@ static hipError_t b3tni_run(const char* name, const void* img, const BL& bl, int
   ProfScope _p(name, st);
   return launch_b3tni(B3EImg{static_cast<const b3_u4*>(img), b3_eimg_cols(Nout)}, bl, q, slab,
                       bslab, Nout, Kout, R, want_bias, st, prev);
-}
-
-template <class BL>
-static hipError_t b3tni_gemm(const char* name, const float* A, int64_t lda, void* img,
-                             const BL& bl, int Nout, int Kout, int R, float* slab, float* bslab,
-                             bool want_bias, TnPlan* plan, hipStream_t st,
-                             int target = kB3TnTarget, const RedJob& prev = RedJob{}) {
-  {
-    ProfScope _p("eimage", st);
-    const hipError_t e = b3_eimage(A, lda, R, Nout, static_cast<b3_u4*>(img), st);
-    if (e != hipSuccess) return e;
-  }
-  return b3tni_run(name, img, bl, Nout, Kout, R, slab, bslab, want_bias, plan, st, target, prev);
 }
 
 // a split-K reduction waiting for its launch: folded into the next side-stream split-bf16 TN
@@ -303,22 +291,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       HIP_RET(launch_b3nt(LdActGradT<ACT_GELU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
     return 0;
   };
-  // capture order: with CGR_RO_MAIN_FIRST=1 (read per call) the fork point is recorded, the main
-  // stream's NT enqueued and the side work after it -- the same dependencies, but in a captured
-  // graph the runtime then keeps the NT on the forward's hardware queue and gives the side
-  // chain the other one (r05 trace: enqueued second, the NT started 11.6 us after the loss
-  // backward, a cross-queue edge on the critical chain)
-  if (ro_main_first() && side != st) {
-    hipEvent_t ro_ev = nullptr;
-    HIP_RET(record_point(ss, st, &ro_ev));
-    if (const int rc = readout_nt()) return rc;
-    HIP_RET(hipStreamWaitEvent(side, ro_ev, 0));
-    if (const int rc = side_readout()) return rc;
-  } else {
-    if (side != st) HIP_RET(fork_to(ss, st, side));
-    if (const int rc = side_readout()) return rc;
-    if (const int rc = readout_nt()) return rc;
-  }
+  // capture order: fork, side work, then the main NT.  Enqueuing the NT first (the fork point
+  // recorded before it, the side work after -- same dependencies) moves the NT onto the forward's
+  // hardware queue in a captured graph but puts the first layer NT beside the readout TN: r05
+  // same-box A/B 344.0k -> 341.0k reactions/s (3 runs each, profiles/r05_ro_first_ab.txt)
+  if (side != st) HIP_RET(fork_to(ss, st, side));
+  if (const int rc = side_readout()) return rc;
+  if (const int rc = readout_nt()) return rc;
 
   // learnable-skip partial-sum slots per layer (bwd_dsig_slots)
   const int nb = WL.dsig_blocks;
@@ -356,7 +335,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     return la;
   };
   // the top layer's weight gradient on the split-bf16 e-image TN takes dpre_{D-1}'s e-image from
-  // the activation kernel that writes dpre_{D-1} (no e-image pass over it)
+  // the activation kernel that writes dpre_{D-1} (no e-image pass over it).  (The layers below
+  // keep the e-image pass: written by the fused layer-backward GEMM's epilogue it cost each such
+  // launch 10 us, step 0.755 -> 0.769 ms, profiles/r05_rejected_epilogue_eimage_*.)
   const bool top_b3 =
       D > 0 && b3tni_ok(LdGatherDiff<false>{fv.a[D - 1], fv.h[D - 1], iv.src_s, iv.rev_s, Hp}, H, E);
   if (D > 0) {  // top layer: dh_D = ds[dst]
@@ -437,8 +418,12 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         mine.splits = p.splits;
         if (const int rc = fold(mine, D - l)) return rc;
       } else if (b3tni_ok(bl, H, E)) {
-        HIP_RET(b3tni_gemm("gemm_tn_wgrad_layer", dp, Hp, img_side, bl, H, H, E, sl, bsl, true,
-                           &p, side, kB3TnTarget, pend.job));
+        {
+          ProfScope _p("eimage", side);
+          HIP_RET(b3_eimage(dp, Hp, E, H, static_cast<b3_u4*>(img_side), side));
+        }
+        HIP_RET(b3tni_run("gemm_tn_wgrad_layer", img_side, bl, H, H, E, sl, bsl, true, &p, side,
+                          kB3TnTarget, pend.job));
         mine.splits = p.splits;
         if (const int rc = fold(mine, D - l)) return rc;
       } else {

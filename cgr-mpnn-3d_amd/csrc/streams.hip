@@ -6,7 +6,7 @@
 #include <mutex>
 #include <string>
 
-#include "ep_bwd.hpp"
+#include "common.hpp"
 #include "gnn_internal.hpp"
 
 namespace cgr {
@@ -22,11 +22,6 @@ bool single_stream() {
     return v && v[0] == '1';
   }();
   return on;
-}
-
-bool ro_main_first() {
-  const char* v = getenv("CGR_RO_MAIN_FIRST");
-  return v && v[0] == '1';
 }
 
 int unpaired_spin_limit() {

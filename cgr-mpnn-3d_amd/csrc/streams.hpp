@@ -37,10 +37,6 @@ SideStreams* side_streams(hipStream_t main);
 // the side streams of `device` if they exist (no creation), else nullptr
 SideStreams* side_streams_of(int device);
 
-// CGR_RO_MAIN_FIRST=1 (read per call; A/B): the backward enqueues its main readout NT before the
-// side stream's first work (gnn_bwd.hip)
-bool ro_main_first();
-
 // CGR_UNPAIRED_SPIN_LIMIT (read per call; tests): the unpaired completers' wait bound in polls
 // (ep_bwd.hpp); negative = report a timeout at once (exercises the error path)
 int unpaired_spin_limit();

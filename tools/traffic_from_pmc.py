@@ -70,6 +70,8 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
     table = {"k_edge_init_seg": "edge_init_seg_fwd", "k_edge_init": "edge_init_fwd",
              "k_layer_bwd": "layer_act_bwd", "k_pool_head": "pool_head_fwd",
              "k_head_bwd": "head_bwd", "k_readout_bwd": "readout_act_bwd",
+             "k_layer_bwd_img": "layer_act_bwd", "k_readout_bwd_img": "readout_act_bwd",
+             "k_b3_segsum_eimage": "segsum_src_bwd",
              "k_reduce_slabs": "splitk_reduce"}
     for k, v in table.items():
         if re.search(r"\b" + k + r"[<(]", n):
