@@ -10,6 +10,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <atomic>
 
@@ -181,5 +182,11 @@ constexpr int kUnpairedSpinLimit = 1 << 22;
 // words of the host-visible error block (pinned host memory mapped into the device, one block per
 // device: streams.hip); plain system-scope stores of 1, never read-modify-write across the bus
 enum : int { kDevErrUnpairedTimeout = 0, kDevErrUnpairedSeen = 1, kDevErrWords = 16 };
+
+// an A/B toggle read per call: VAR=1 in the environment
+inline bool getenv_flag(const char* var) {
+  const char* v = getenv(var);
+  return v && v[0] == '1';
+}
 
 }  // namespace cgr

@@ -337,7 +337,9 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // the top layer's weight gradient on the split-bf16 e-image TN takes dpre_{D-1}'s e-image from
   // the activation kernel that writes dpre_{D-1} (no e-image pass over it).  (The layers below
   // keep the e-image pass: written by the fused layer-backward GEMM's epilogue it cost each such
-  // launch 10 us, step 0.755 -> 0.769 ms, profiles/r05_rejected_epilogue_eimage_*.)
+  // launch 10 us, step 0.755 -> 0.769 ms, profiles/r05_rejected_epilogue_eimage_*.  Against
+  // the top layer's pass on the side stream: same-box A/B 341.6k vs 341.1k reactions/s,
+  // profiles/r05_ab2_top_eimage_fused_vs_side.txt.)
   const bool top_b3 =
       D > 0 && b3tni_ok(LdGatherDiff<false>{fv.a[D - 1], fv.h[D - 1], iv.src_s, iv.rev_s, Hp}, H, E);
   if (D > 0) {  // top layer: dh_D = ds[dst]

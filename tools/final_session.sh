@@ -19,7 +19,7 @@ tail -2 "$OUT/pytest_gpu.txt"; [ $rc -eq 0 ] || exit 1
 st "bench cfg2 (defaults)"
 timeout -k 10 400 python bench.py > "$OUT/bench_cfg2.json" 2> "$OUT/bench_cfg2.err" || exit 1
 python -c "import json; d=json.loads(open('$OUT/bench_cfg2.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['kernel'], d['roofline']['frac'])"
-for c in cfg4 cfg5 train_default; do
+for c in ${CONFIGS:-cfg4 cfg5 train_default sweep_b16 sweep_b64}; do
   st "bench $c"
   timeout -k 10 300 python bench.py --config $c --cpu-baseline 0 > "$OUT/bench_$c.json" 2> "$OUT/bench_$c.err" || exit 1
   python -c "import json; d=json.loads(open('$OUT/bench_$c.json').read().strip().splitlines()[-1]); print('$c', d['value'], d['ms_per_step'])"
@@ -30,5 +30,7 @@ if [ "${SKIP_PROF:-0}" = "0" ]; then
     -- python bench.py --cpu-baseline 0 > "$OUT/prof_bench.json" 2> "$OUT/prof_bench.err" || exit 1
   st "PMC passes"
   TAG=$TAG bash tools/pmc_profile.sh || exit 1
+  st "scatter-add PMC passes"
+  TAG=$TAG-scatter bash tools/scatter_pmc.sh > "$OUT/scatter_pmc.log" 2>&1 || exit 1
 fi
 st done
