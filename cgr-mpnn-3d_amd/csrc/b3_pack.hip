@@ -151,7 +151,7 @@ hipError_t b3_eimage(const float* x, int64_t ld, int64_t R, int C, b3_u4* img, h
 // e-image of the segmented sum G[v, :C] = sum_{j in [ptr[v], ptr[v+1])} X[idx[j], :C] (the node
 // weight gradient's Gs = segsum_src(dpre0), gnn_bwd.hip) without G ever reaching memory.  Block =
 // one 32-row step s x 64 columns: the sums (thread = (row, float4 column), the segment's rows in
-// order, as k_segsum_v4 adds them) go to an LDS tile [32][65], then thread = (column, 8-row chunk),
+// order, as k_segsum_v4m adds them) go to an LDS tile [32][65], then thread = (column, 8-row chunk),
 // chunk fastest, splits its 8 values and writes the two 16-byte chunk slots (a wave's stores cover
 // 16 consecutive 64-byte slots).  Rows >= R and columns >= C are written as 0.
 constexpr int kSegImgCols = 64;

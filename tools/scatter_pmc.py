@@ -4,7 +4,7 @@
     python tools/scatter_pmc.py collect gpurun_out/<tag> [profiles/traffic.json] [cfg2]
 
 `run` builds the cfg2 bench batch and launches cgr_segment_sum 5 + 50 times per kernel (the dst
-scatter, k_segsum_v4<false>, and its src-gather twin, <true>) in the given cache state.
+scatter, k_segsum_v4m<false, 2>, and its src-gather twin, <true, 2>) in the given cache state.
 `collect` reads the FETCH_SIZE / WRITE_SIZE passes, drops each kernel's first 5 dispatches
 (warm-up) and writes per-launch HBM bytes, (2 FETCH_SIZE + WRITE_SIZE) x 1024 (gfx950 calibration,
 MI355X_MICROARCH.md HBM section), into traffic.json under segsum_dst_fwd (warm),
@@ -17,6 +17,7 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -52,7 +53,7 @@ def collect(root, out_path=None, cfg="cfg2"):
                 for r in rows:
                     per.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
             for name, v in per.items():
-                kind = "src" if "<true>" in name else "dst"
+                kind = "src" if re.search(r"k_segsum\w*<true", name) else "dst"
                 v = v[5:]  # warm-up dispatches
                 vals.setdefault(kind, {})[counter] = sum(v) / max(1, len(v))
                 vals[kind]["n"] = len(v)

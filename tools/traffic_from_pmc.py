@@ -66,7 +66,7 @@ def classify(name: str, grid: int, grids_by_name: dict) -> str | None:
             return "gemm_tn_wgrad_node"
         return "gemm_tn_wgrad_edge"  # ambiguous only when F % 4 == 0; see note in the output
     if "k_segsum" in n:
-        return "segsum_src_bwd" if "<true>" in n else "segsum_dst_fwd"
+        return "segsum_src_bwd" if re.search(r"k_segsum\w*<true", n) else "segsum_dst_fwd"
     table = {"k_edge_init_seg": "edge_init_seg_fwd", "k_edge_init": "edge_init_fwd",
              "k_layer_bwd": "layer_act_bwd", "k_pool_head": "pool_head_fwd",
              "k_head_bwd": "head_bwd", "k_readout_bwd": "readout_act_bwd",
