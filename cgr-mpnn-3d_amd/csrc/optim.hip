@@ -27,7 +27,10 @@ struct AdamHyper {
 };
 
 constexpr int kAdamThreads = 256;
-constexpr int kAdamElemsPerBlock = kAdamThreads * 4 * 4;  // 4 float4 per thread
+// one float4 per thread: 1.49 M parameters at cfg2 make ~1,460 blocks, every element's five loads
+// in flight at once (r04's 16 elements per thread gave 91 blocks on 256 CUs: 15.4 us in the
+// replayed step for 54 MB)
+constexpr int kAdamElemsPerBlock = kAdamThreads * 4;
 
 // t <- t + 1 for every tensor of the group (before k_adam reads it, same stream)
 __global__ void k_adam_step_count(AdamGroup G) {
@@ -57,11 +60,17 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamGroup G, AdamHyper h)
   const int b = blockIdx.x;
   int t = 0;
   while (t + 1 < G.n && G.first_block[t + 1] <= b) ++t;
-  const double step = (double)G.step[t][0];
-  const double bc1 = 1.0 - pow(h.b1, step);
-  const double bc2 = 1.0 - pow(h.b2, step);
-  const float neg_step_size = (float)(-(h.lr / bc1));
-  const float bc2_sqrt = (float)sqrt(bc2);
+  // the bias corrections once per block (double pow), broadcast through LDS
+  __shared__ float sc[2];
+  if (threadIdx.x == 0) {
+    const double step = (double)G.step[t][0];
+    const double bc1 = 1.0 - pow(h.b1, step);
+    const double bc2 = 1.0 - pow(h.b2, step);
+    sc[0] = (float)(-(h.lr / bc1));
+    sc[1] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const float neg_step_size = sc[0], bc2_sqrt = sc[1];
   const int64_t base = (int64_t)(b - G.first_block[t]) * kAdamElemsPerBlock;
   const int64_t n = G.numel[t];
   float* P = G.p[t];
@@ -69,36 +78,23 @@ __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamGroup G, AdamHyper h)
   float* M = G.m[t];
   float* V = G.v[t];
   float* VM = G.vmax[t];
-  if (G.vec4[t]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t e = base + 4 * ((int64_t)i * kAdamThreads + threadIdx.x);
-      if (e + 4 <= n) {
-        float4 p4 = *reinterpret_cast<const float4*>(P + e);
-        const float4 g4 = *reinterpret_cast<const float4*>(Gr + e);
-        float4 m4 = *reinterpret_cast<const float4*>(M + e);
-        float4 v4 = *reinterpret_cast<const float4*>(V + e);
-        float4 x4 = h.amsgrad ? *reinterpret_cast<const float4*>(VM + e) : v4;
-        adam_elem(p4.x, g4.x, m4.x, v4.x, x4.x, h, neg_step_size, bc2_sqrt);
-        adam_elem(p4.y, g4.y, m4.y, v4.y, x4.y, h, neg_step_size, bc2_sqrt);
-        adam_elem(p4.z, g4.z, m4.z, v4.z, x4.z, h, neg_step_size, bc2_sqrt);
-        adam_elem(p4.w, g4.w, m4.w, v4.w, x4.w, h, neg_step_size, bc2_sqrt);
-        *reinterpret_cast<float4*>(P + e) = p4;
-        *reinterpret_cast<float4*>(M + e) = m4;
-        *reinterpret_cast<float4*>(V + e) = v4;
-        if (h.amsgrad) *reinterpret_cast<float4*>(VM + e) = x4;
-      } else {
-        for (int64_t k = e; k < n && k < e + 4; ++k) {
-          float vm = h.amsgrad ? VM[k] : 0.f;
-          adam_elem(P[k], Gr[k], M[k], V[k], vm, h, neg_step_size, bc2_sqrt);
-          if (h.amsgrad) VM[k] = vm;
-        }
-      }
-    }
+  const int64_t e = base + 4 * (int64_t)threadIdx.x;
+  if (G.vec4[t] && e + 4 <= n) {
+    float4 p4 = *reinterpret_cast<const float4*>(P + e);
+    const float4 g4 = *reinterpret_cast<const float4*>(Gr + e);
+    float4 m4 = *reinterpret_cast<const float4*>(M + e);
+    float4 v4 = *reinterpret_cast<const float4*>(V + e);
+    float4 x4 = h.amsgrad ? *reinterpret_cast<const float4*>(VM + e) : v4;
+    adam_elem(p4.x, g4.x, m4.x, v4.x, x4.x, h, neg_step_size, bc2_sqrt);
+    adam_elem(p4.y, g4.y, m4.y, v4.y, x4.y, h, neg_step_size, bc2_sqrt);
+    adam_elem(p4.z, g4.z, m4.z, v4.z, x4.z, h, neg_step_size, bc2_sqrt);
+    adam_elem(p4.w, g4.w, m4.w, v4.w, x4.w, h, neg_step_size, bc2_sqrt);
+    *reinterpret_cast<float4*>(P + e) = p4;
+    *reinterpret_cast<float4*>(M + e) = m4;
+    *reinterpret_cast<float4*>(V + e) = v4;
+    if (h.amsgrad) *reinterpret_cast<float4*>(VM + e) = x4;
   } else {
-    for (int i = 0; i < 16; ++i) {
-      const int64_t k = base + (int64_t)i * kAdamThreads + threadIdx.x;
-      if (k >= n) break;
+    for (int64_t k = e; k < n && k < e + 4; ++k) {
       float vm = h.amsgrad ? VM[k] : 0.f;
       adam_elem(P[k], Gr[k], M[k], V[k], vm, h, neg_step_size, bc2_sqrt);
       if (h.amsgrad) VM[k] = vm;

@@ -17,7 +17,7 @@ else
   git -C "$ROOT" worktree add --detach "$SRC" "$REV" > /dev/null
   trap 'git -C "$ROOT" worktree remove --force "$SRC"' EXIT
 fi
-make -C "$SRC/cgr-mpnn-3d_amd/csrc" -j8 OUTDIR="$ROOT/build/variants/$NAME" OBJDIR="$OBJ" \
+make -C "$SRC/cgr-mpnn-3d_amd/csrc" -j8 OUTDIR="$ROOT/${VARIANT_ROOT:-build/variants}/$NAME" OBJDIR="$OBJ" \
   EXTRA="$EXTRA" > /dev/null
 rm -rf "$OBJ"
-ls -la "$ROOT/build/variants/$NAME/libcgr_mpnn3d.so"
+ls -la "$ROOT/${VARIANT_ROOT:-build/variants}/$NAME/libcgr_mpnn3d.so"
