@@ -1035,13 +1035,6 @@ hipError_t b3_segsum_eimage(const float* x, int64_t ld, const int* idx, const in
 //   * bias (column sums of A) from the pieces, hi + lo per element: n-fragment f is summed by
 //     the k-tile min(f / TNK, tiles_k - 1), inside the compute wave that loads f (the remainder
 //     fragments by the wave holding their k-fragment-0 product).
-// The e-image TN's pipeline: one barrier per two k steps (1) or per step (0).  Per step the
-// compute and staging waves each worked ~14 us of a 22 us loop and waited ~8 at the barriers
-// (r04 phase stamps, cfg2 layer shape): pairing steps lets one step's slack absorb the other's.
-#ifndef CGR_TNI_PAIR
-#define CGR_TNI_PAIR 1
-#endif
-
 template <int TNN, int TNK>
 struct B3TniShape {
   static constexpr int CW = 8;
@@ -1055,9 +1048,7 @@ struct B3TniShape {
   static constexpr int RX = (REM + CW - 1) / CW;
   static constexpr int NA = RN + RX;        // A fragments a compute wave loads per step
   static constexpr int SU4 = 2 * BC * 4;    // b3_u4 per LDS stage buffer
-  // two steps per barrier interval (CGR_TNI_PAIR, r05): four stage buffers, else two
-  static constexpr int NBUF = CGR_TNI_PAIR ? 4 : 2;
-  static constexpr size_t LDS_BYTES = (size_t)NBUF * SU4 * 16;
+  static constexpr size_t LDS_BYTES = (size_t)2 * SU4 * 16;
 };
 
 // prev (slab == null: none): the previous weight gradient's split-K slabs, reduced by this
@@ -1124,22 +1115,9 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
       const int e = e_begin + t * 32 + 4 * hc + j;
       return e < R ? e : 0;
     };
-    auto index_to = [&](int t, int (&ixs)[4][2]) {  // the gather's index loads of step t
+    auto index = [&](int t) {  // the gather's index loads of step t
 #pragma unroll
-      for (int j = 0; j < 4; ++j) TB::idx(bl, rowof(t, j), ixs[j]);
-    };
-    auto index = [&](int t) { index_to(t, ix); };
-    auto fetch_from = [&](float4 (&raw)[16], const int (&ixs)[4][2]) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int h = 0; h < TB::NL / 8; ++h) off[8 * h + j] = TB::off(bl, ixs[j], h, gcol, Kout);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) raw[i] = *reinterpret_cast<const float4*>(base0 + off[i]);
-      if constexpr (TB::NL == 16) {
-#pragma unroll
-        for (int i = 8; i < 12; ++i) raw[i] = *reinterpret_cast<const float4*>(base1 + off[i]);
-      }
+      for (int j = 0; j < 4; ++j) TB::idx(bl, rowof(t, j), ix[j]);
     };
     auto fetch = [&](float4 (&raw)[16]) {  // addresses from the last index(), then the loads
 #pragma unroll
@@ -1176,36 +1154,7 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
         put(img, 3, u[0].w, u[1].w, u[2].w, u[3].w);
       }
     };
-    if (CGR_TNI_PAIR && nt > 0) {
-      // interval u computes steps 2u, 2u + 1 (buffers 2u % 4, (2u + 1) % 4) while this stages
-      // steps 2u + 2, 2u + 3, loaded during interval u - 1; index sets one interval ahead
-      int ixb[4][2];
-      index_to(0, ix);
-      fetch_from(raw0, ix);  // step 0
-      index_to(1, ixb);
-      fetch_from(raw1, ixb);  // step 1
-      index_to(2, ix);
-      index_to(3, ixb);
-      stage(raw0, 0);
-      stage(raw1, 1);
-      fetch_from(raw0, ix);   // step 2
-      fetch_from(raw1, ixb);  // step 3
-      index_to(4, ix);
-      index_to(5, ixb);
-      __syncthreads();
-      TN_STAMP_START();
-      for (int t = 0; t < nt; t += 2) {
-        if (t + 2 < nt) stage(raw0, (t + 2) & 3);
-        if (t + 3 < nt) stage(raw1, (t + 3) & 3);
-        fetch_from(raw0, ix);   // step t + 4
-        fetch_from(raw1, ixb);  // step t + 5
-        index_to(t + 6, ix);
-        index_to(t + 7, ixb);
-        TN_STAMP_PRE();
-        __syncthreads();
-        TN_STAMP_POST();
-      }
-    } else if (nt > 0) {
+    if (nt > 0) {
       index(0);
       fetch(raw0);  // step 0
       index(1);
@@ -1321,25 +1270,7 @@ __global__ __launch_bounds__((B3TniShape<TNN, TNK>::NT)) void gemm_b3tni_kernel(
         bsum[f] += s;
       }
   };
-  if (CGR_TNI_PAIR && nt > 0) {
-    b3_u4 a0[NA][2], a1[NA][2];
-    aload(0, a0);
-    __syncthreads();  // B(0), B(1) staged
-    TN_STAMP_START();
-    for (int t = 0; t < nt; t += 2) {
-      aload(t + 1, a1);
-      __builtin_amdgcn_sched_barrier(0);
-      compute(t & 3, a0);
-      if (t + 1 < nt) {
-        aload(t + 2, a0);
-        __builtin_amdgcn_sched_barrier(0);
-        compute((t + 1) & 3, a1);
-      }
-      TN_STAMP_PRE();
-      __syncthreads();
-      TN_STAMP_POST();
-    }
-  } else if (nt > 0) {
+  if (nt > 0) {
     b3_u4 a0[NA][2], a1[NA][2];
     aload(0, a0);
     __syncthreads();  // B(0) staged
