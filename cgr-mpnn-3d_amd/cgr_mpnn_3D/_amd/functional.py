@@ -100,9 +100,12 @@ class GNNFunction(torch.autograd.Function):
         ptab = _param_table(params)
         dps = _dropout_array(dropout_ps, cfg.depth)
         # CGR_TRAIN_DROPOUT | CGR_TRAIN_FOR_BACKWARD (include/cgr_mpnn3d.h): the backward's
-        # weight-gradient operands are prepared only when a parameter gradient is wanted
+        # weight-gradient operands are prepared only when a gradient is wanted (parameters, or
+        # x / edge_attr: the input gradients come after the parameter backward)
+        want_bwd = any(ctx.needs_input_grad[12:]) or ctx.needs_input_grad[1] or \
+            ctx.needs_input_grad[3]
         flags = (native.TRAIN_DROPOUT if training else 0) | (
-            native.TRAIN_FOR_BACKWARD if any(ctx.needs_input_grad[12:]) else 0)
+            native.TRAIN_FOR_BACKWARD if want_bwd else 0)
         with native.device_guard(dev):
             native.check(lib.cgr_gnn_forward(ctypes.byref(cfg), ptab, ctypes.byref(bs), dps,
                                              ctypes.c_uint64(seed), native.ptr(rng_counter),
@@ -150,11 +153,25 @@ class GNNFunction(torch.autograd.Function):
                 _dropout_array(ctx.dropout_ps, cfg.depth), ctypes.c_uint64(ctx.seed),
                 ctx.flags, native.ptr(arena), native.ptr(dy), _param_table(grads),
                 native.ptr(ws), evtab, native.stream_ptr(dev)))
+        dx = dea = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[3]:
+            # x.grad / edge_attr.grad (GNN.py:85-86,105-106): from what the backward left in `ws`
+            if ctx.needs_input_grad[1]:
+                dx = torch.empty(x.shape, dtype=torch.float32, device=dev)
+            if ctx.needs_input_grad[3]:
+                dea = torch.empty(edge_attr.shape, dtype=torch.float32, device=dev)
+            with native.device_guard(dev):
+                native.check(lib.cgr_gnn_input_grads(
+                    ctypes.byref(cfg), _param_table(params), ctypes.byref(bs), native.ptr(arena),
+                    native.ptr(dy), native.ptr(ws),
+                    native.ptr(dx) if dx is not None and dx.numel() else None,
+                    native.ptr(dea) if dea is not None and dea.numel() else None,
+                    native.stream_ptr(dev)))
         if hook is not None:
             # e.g. the RCCL all-reduce of every bucket, each started as soon as its event fires
             # (cgr_mpnn_3D._amd.ddp); must leave the current stream ordered after its work
             hook(flat, buckets, events)
-        return (None,) * 12 + tuple(grads)
+        return (None, dx, None, dea) + (None,) * 8 + tuple(grads)
 
 
 def gnn_predict(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, dropout_ps,

@@ -15,7 +15,7 @@ _LIB_NAME = "libcgr_mpnn3d.so"
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CGR_MPNN3D_LIB", os.path.join(_HERE, "lib", _LIB_NAME))
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 TRAIN_DROPOUT, TRAIN_FOR_BACKWARD = 1, 2  # cgr_gnn_forward / _backward `training` bits
 MAX_DEPTH = 32
 ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
@@ -76,6 +76,9 @@ SIGNATURES = [
     ("cgr_gnn_backward", c_int32,
      [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), POINTER(c_float), c_uint64,
       c_int32, c_void_p, c_void_p, POINTER(c_void_p), c_void_p, POINTER(c_void_p), c_void_p]),
+    ("cgr_gnn_input_grads", c_int32,
+     [POINTER(CgrGnnConfig), POINTER(c_void_p), POINTER(CgrBatch), c_void_p, c_void_p, c_void_p,
+      c_void_p, c_void_p, c_void_p]),
     ("cgr_gnn_image_bytes", c_int64, [POINTER(CgrGnnConfig)]),
     ("cgr_gnn_pack_images", c_int32, [POINTER(CgrGnnConfig), POINTER(c_void_p), c_void_p,
                                       c_void_p]),

@@ -190,11 +190,6 @@ class GNN(nn.Module):
         drop = [float(self.dropout_ps[l]) for l in range(self.depth)]  # IndexError like GNN.py:101
 
         dev = x.device
-        if torch.is_grad_enabled() and (x.requires_grad or (
-                edge_attr is not None and edge_attr.requires_grad)):
-            raise NotImplementedError(
-                "cgr_mpnn_3D (MI355X): gradients with respect to x / edge_attr are not produced "
-                "by the native backward (parameters only); detach the inputs")
         x = x.to(dtype=torch.float32).contiguous()
         edge_index = edge_index.to(device=dev, dtype=torch.int64).contiguous()
         F_ = x.shape[1]
@@ -253,7 +248,9 @@ class GNN(nn.Module):
             counter = self._cgr_rng_counter = counter.to(dev)
         cfg = (F_, Fe, H, self.depth, act, self.use_learnable_skip)
         params = [p.contiguous() for p in params]
-        if not (torch.is_grad_enabled() and any(p.requires_grad for p in params)):
+        want_grad = any(p.requires_grad for p in params) or x.requires_grad or \
+            edge_attr.requires_grad
+        if not (torch.is_grad_enabled() and want_grad):
             # no gradient wanted (test.py / the CLI run under torch.no_grad()): the forward-only
             # path, no saved activations
             return gnn_predict(cfg, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, drop,

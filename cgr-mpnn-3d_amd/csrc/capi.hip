@@ -42,6 +42,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
                       const float* dropout_p, uint64_t seed, int training, const void* arena,
                       const float* dy, float* const* grads, void* workspace,
                       hipEvent_t const* bucket_events, hipStream_t st);
+int gnn_input_grads_impl(const Dims& d, const float* const* params, const void* arena,
+                         const float* dy, void* workspace, float* dx, float* de, hipStream_t st);
 
 Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
   Dims d;
@@ -307,6 +309,7 @@ WorkspaceLayout workspace_layout(const Dims& d) {
   // segment tickets, then one unpaired grid counter per fused layer-backward launch
   W.cnt = b.take(4 * (N * (size_t)layer_cols(d).tiles + CGR_MAX_DEPTH));
   W.part = b.take(4 * (size_t)bwd_seg_tiles(d) * 2 * (size_t)layer_cols(d).nf * 16);
+  W.wxT = b.take(4 * (size_t)d.F * (size_t)input_grad_ldw(d.H));
   W.dsig_blocks = bwd_dsig_slots(d);
   W.dsig_part = b.take(4 * (size_t)d.D * (size_t)W.dsig_blocks);
   W.bytes = b.off;
@@ -463,6 +466,29 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, cons
   return gnn_backward_impl(d, params, b, dropout_p, seed, training, arena, dy, grads, workspace,
                            reinterpret_cast<hipEvent_t const*>(bucket_events),
                            (hipStream_t)stream);
+}
+
+int cgr_gnn_input_grads(const cgr_gnn_config* cfg, const float* const* params,
+                        const cgr_batch* b, const void* arena, const float* dy, void* workspace,
+                        float* dx, float* dedge_attr, void* stream) {
+  clear_stale_hip_error();
+  int rc = validate_config(cfg);
+  if (rc) return rc;
+  rc = validate_batch(cfg, b);
+  if (rc) return rc;
+  CGR_CHECK(params != nullptr && arena != nullptr && dy != nullptr && workspace != nullptr,
+            "cgr: params / arena / dy / workspace must not be NULL");
+  const int ff = forward_flags(arena);
+  CGR_CHECK(ff >= 0 && (ff & CGR_TRAIN_FOR_BACKWARD),
+            "cgr_gnn_input_grads: `arena` was not filled by a successful cgr_gnn_forward with "
+            "CGR_TRAIN_FOR_BACKWARD set");
+  CGR_CHECK(((uintptr_t)dx & 15) == 0 && ((uintptr_t)dedge_attr & 15) == 0,
+            "cgr_gnn_input_grads: dx / dedge_attr must be 16-byte aligned (or NULL)");
+  const int np = cgr_gnn_num_params(cfg);
+  for (int i = 0; i < np; ++i) CGR_CHECK(params[i] != nullptr, "cgr: NULL parameter pointer");
+  const Dims d = make_dims(cfg, b->num_nodes, b->num_edges, b->num_graphs);
+  return gnn_input_grads_impl(d, params, arena, dy, workspace, dx, dedge_attr,
+                              (hipStream_t)stream);
 }
 
 int64_t cgr_gnn_image_bytes(const cgr_gnn_config* cfg) {

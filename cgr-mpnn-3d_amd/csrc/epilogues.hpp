@@ -62,6 +62,34 @@ struct EpStore {
   }
 };
 
+// C[rows[r], :] = acc: output rows scattered through a permutation (the edge-feature input
+// gradient: sorted edge position r -> the caller's edge id perm[r]).  C is the caller's [M, N]
+// tensor (any N: scalar stores unless the row is float4-aligned).
+struct EpStorePermRows {
+  static constexpr bool kSeg = false;
+  float* C;
+  int64_t ld;
+  int M, N;
+  const int* rows;
+  struct Ctx {};
+  __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
+  __device__ __forceinline__ void finish_ctx(Ctx&) const {}
+  typedef int Pre;
+  __device__ __forceinline__ Pre pre4(int r, int) const { return rows[min(r, M - 1)]; }
+  __device__ __forceinline__ void apply4p(int r, int c, float4 v, Pre pr, const Ctx&) const {
+    if (r >= M || c >= N) return;
+    float* o = C + (int64_t)pr * ld + c;
+    if (c + 4 <= N && (ld & 3) == 0 && ((uintptr_t)C & 15) == 0) {
+      *reinterpret_cast<float4*>(o) = v;
+    } else {
+      o[0] = v.x;
+      if (c + 1 < N) o[1] = v.y;
+      if (c + 2 < N) o[2] = v.z;
+      if (c + 3 < N) o[3] = v.w;
+    }
+  }
+};
+
 // C[r, :] = s_r * acc with s_r = dy[node_graph[r]] (readout backward ds = dzn W_n[:, F:], the
 // row factor of dzn; LdActGrad).  Internal [M, ld] buffers, ld % 4 == 0.
 struct EpStoreRowScale {

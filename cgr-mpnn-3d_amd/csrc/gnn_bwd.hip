@@ -538,4 +538,60 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   return 0;
 }
 
+// Input gradients (autograd's x.grad / edge_attr.grad for the reference, GNN.py:85-86,105-106):
+// x enters edge_init through x[src] and edge_to_node through [x | s], edge_attr edge_init only:
+//   dq0 = dpre0 W0                     (q0 = [x[src] | e], GNN.py:86)
+//   dx  = segsum_src(dpre0) W0[:, :F] + dzn W_n[:, :F]  = [Gs | dzn] [W0x ; W_nx]
+//   de  = dpre0 W0[:, F:]              (rows back to the caller's edge order through perm)
+// dpre0 is what gnn_backward_impl left in the workspace's dh0 buffer; Gs and dzn are re-formed
+// in fp32 (the backward keeps them as e-images only) and the stacked weight slices transposed
+// into wxT, so both products are one fp32 MFMA NT launch each (gemm.hpp), exact-fp32 products.
+int gnn_input_grads_impl(const Dims& d, const float* const* params, const void* arena,
+                         const float* dy, void* workspace, float* dx, float* de, hipStream_t st) {
+  const ArenaLayout L = arena_layout(d);
+  const IndexView iv = index_view(const_cast<void*>(arena), L);
+  const FloatView fv = float_view(const_cast<void*>(arena), L, d);
+  const WorkspaceLayout WL = workspace_layout(d);
+  char* ws = static_cast<char*>(workspace);
+  const float* dpre0 = reinterpret_cast<const float*>(ws + WL.dh0);
+  const int N = (int)d.N, E = (int)d.E, H = d.H, Hp = d.Hp, F = d.F, Fe = d.Fe, D = d.D;
+  if (de && Fe > 0) {  // de = dpre0 W0e: B = W0[:, F:]^T, the forward's w0eT [Fe, Hp]
+    ProfScope _p("input_grad_edge", st);
+    const LdPlain<4> al{dpre0, Hp};
+    const LdPlain<4> bl{fv.w0eT, Hp};
+    const EpStorePermRows ep{de, Fe, E, Fe, iv.perm};
+    HIP_RET(with_nt_rn(Fe, [&](auto RN) {
+      return launch_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, E, Fe, H, st);
+    }));
+  }
+  if (dx && F > 0) {
+    float* Gs = reinterpret_cast<float*>(ws + WL.Gs);
+    float* dzn = reinterpret_cast<float*>(ws + WL.dzn);
+    float* wxT = reinterpret_cast<float*>(ws + WL.wxT);
+    const int ldw = input_grad_ldw(H);
+    {
+      ProfScope _p("input_grad_prep", st);
+      HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, H, Gs, Hp, st));
+      HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
+                              Hp, d.act, dzn, nullptr, st));
+      TransposeJobs tj{};  // wxT [F, ldw] = [W0[:, :F]^T | W_n[:, :F]^T]
+      tj.job[0] = TransposeJob{params[CGR_PARAM_EDGE_INIT_W], F + Fe, 0, wxT, ldw, H, F};
+      tj.job[1] = TransposeJob{params[CGR_PARAM_E2N_W(D)], F + H, 0, wxT + H, ldw, H, F};
+      tj.n = 2;
+      HIP_RET(transpose_batch(tj, st));
+    }
+    ProfScope _p("input_grad_node", st);
+    const LdPlain<4> bl{wxT, ldw};
+    const EpStore ep{dx, F, N, F, nullptr};
+    // [Gs | dzn] rows: the concat boundary H must not split a VEC-wide chunk
+    HIP_RET(with_vec(H % 4 == 0 ? 4 : (H % 2 == 0 ? 2 : 1), [&](auto V) {
+      const LdConcat<decltype(V)::value> al{Gs, Hp, dzn, Hp, H};
+      return with_nt_rn(F, [&](auto RN) {
+        return launch_nt<4, 1, decltype(RN)::value, 1>(al, bl, ep, N, F, 2 * H, st);
+      });
+    }));
+  }
+  return 0;
+}
+
 }  // namespace cgr

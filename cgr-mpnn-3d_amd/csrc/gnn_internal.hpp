@@ -127,8 +127,12 @@ struct WorkspaceLayout {
   size_t cnt;
   // [row tiles * column tiles, 2, BN] partial sums of the segments over >= 3 row tiles
   size_t part;
+  // [F, input_grad_ldw(H)] the stacked, transposed x slices of edge_init / edge_to_node weights
+  // (cgr_gnn_input_grads only)
+  size_t wxT;
   int dsig_blocks;
 };
+inline int input_grad_ldw(int H) { return (2 * H + 3) & ~3; }
 int bwd_dsig_slots(const Dims& d);
 int bwd_seg_tiles(const Dims& d);
 struct B3Cols;

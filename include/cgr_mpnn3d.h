@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define CGR_ABI_VERSION 5
+#define CGR_ABI_VERSION 6
 #define CGR_MAX_DEPTH 32
 
 enum cgr_status {
@@ -148,6 +148,18 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params,
                      const cgr_batch* batch, const float* dropout_p, uint64_t seed,
                      int32_t training, const void* arena, const float* dy, float* const* grads,
                      void* workspace, void* const* bucket_events, void* stream);
+
+/* Gradients with respect to the inputs (what autograd gives the reference for x / edge_attr
+ * tensors that require grad: x enters through x[row] in edge_init, GNN.py:85-86, and through
+ * cat([x, s]) in edge_to_node, GNN.py:105-106; edge_attr through edge_init only).  Call after
+ * cgr_gnn_backward, on the same stream, with the same config / params / batch / arena / dy and
+ * the SAME workspace (it reads the edge-init pre-activation gradient that backward left there).
+ * dx: device [num_nodes, num_node_features] (NULL: skipped); dedge_attr: device
+ * [num_edges, num_edge_features] in the caller's edge order (NULL: skipped); both overwritten,
+ * fp32, 16-byte aligned. */
+int cgr_gnn_input_grads(const cgr_gnn_config* cfg, const float* const* params,
+                        const cgr_batch* batch, const void* arena, const float* dy,
+                        void* workspace, float* dx, float* dedge_attr, void* stream);
 
 /* Forward-only inference (test.py:85-113 and cli_tool/activation_energy_predictor.py:70-80 run
  * GNN.forward under torch.no_grad() in eval mode).  cgr_gnn_predict computes exactly what

@@ -18,7 +18,10 @@ What is restated (reference = tobjec/CGR-MPNN-3D @ 2025-02-27):
                           (``propagate`` ``GNN.py:134`` / ``global_add_pool`` ``GNN.py:110``)
                           restated as a sparse incidence product, ``dim_size = N``.
 * ``backward``            hand-derived reverse mode of the above, the exact
-                          sequence the HIP backward kernels implement.
+                          sequence the HIP backward kernels implement; with ``inputs_out`` also
+                          the gradients w.r.t. ``x`` (through ``x[row]``, ``GNN.py:85-86``, and
+                          ``cat([x, s])``, ``GNN.py:105-106``) and ``edge_attr`` (``GNN.py:86``),
+                          pinned by the goldens' ``gin_*`` arrays (reference autograd).
 """
 
 from __future__ import annotations
@@ -188,8 +191,9 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     return y, cache
 
 
-def backward(params: dict, cache: dict, dy: np.ndarray) -> dict:
-    """Reverse mode of ``forward``. Returns grads keyed like ``state_dict``."""
+def backward(params: dict, cache: dict, dy: np.ndarray, inputs_out: dict | None = None) -> dict:
+    """Reverse mode of ``forward``. Returns grads keyed like ``state_dict``.
+    ``inputs_out`` (a dict, optional) receives ``"x"`` [N, F] and ``"edge_attr"`` [E, Fe]."""
     f8 = np.float64
     act = cache["act"]
     D = cache["depth"]
@@ -240,18 +244,26 @@ def backward(params: dict, cache: dict, dy: np.ndarray) -> dict:
     dz0 = dh0 * grad_of(cache["z0"], "z0")
     grads["edge_init.weight"] = dz0.T @ cache["q0"]
     grads["edge_init.bias"] = dz0.sum(0)
+    if inputs_out is not None:
+        # q0 = [x[src] | e] (GNN.py:86): dq0 = dz0 W0; x[src] -> scatter at src; q = [x | s]
+        dq0 = dz0 @ np.asarray(params["edge_init.weight"], f8)
+        dx = _scatter_sum(dq0[:, :F_], src, N) + dzn @ Wn[:, :F_]
+        inputs_out["x"] = dx
+        inputs_out["edge_attr"] = dq0[:, F_:]
     return grads
 
 
 def loss_and_grads(params, x, edge_index, edge_attr, batch, y_true, depth, act="relu",
-                   learnable_skip=False, num_graphs=None, relu_masks=None, cache_out=None):
+                   learnable_skip=False, num_graphs=None, relu_masks=None, cache_out=None,
+                   inputs_out=None):
     """MSELoss(reduction='sum') (train.py:120) forward + backward: (loss, y_hat, grads).
-    `cache_out` (a dict, optional) receives the forward / backward cache (incl. "skip_abs")."""
+    `cache_out` (a dict, optional) receives the forward / backward cache (incl. "skip_abs");
+    `inputs_out` (a dict, optional) the input gradients (``backward``)."""
     y, cache = forward(params, x, edge_index, edge_attr, batch, depth, act, learnable_skip,
                        num_graphs, relu_masks=relu_masks)
     r = y - np.asarray(y_true, np.float64)
     loss = float((r * r).sum())
-    grads = backward(params, cache, 2.0 * r)
+    grads = backward(params, cache, 2.0 * r, inputs_out)
     if cache_out is not None:
         cache_out.update(cache)
     return loss, y, grads

@@ -13,7 +13,8 @@ in ``sys.modules`` first:
 Both use ``Tensor.scatter_add_`` exactly as PyG's ``utils.scatter(reduce='sum')`` does.
 
 Outputs: ``tests/golden/<case>.npz`` holding inputs, the ``state_dict``, eval-mode predictions,
-the train-mode (dropout p=0) ``MSELoss(sum)`` loss and every parameter gradient.  Only these data
+the train-mode (dropout p=0) ``MSELoss(sum)`` loss, every parameter gradient and the gradients
+with respect to ``x`` / ``edge_attr`` (``gin_*``).  Only these data
 files are committed; the reference itself never leaves this container.
 
     python tests/golden/make_golden.py
@@ -152,7 +153,11 @@ def run_case(ref, name, bkw, mkw, extra):
     model.dropout_ps = [0.0] * D
     model.train()
     model.zero_grad()
-    pred = model(data)
+    # inputs that require grad: autograd's x.grad / edge_attr.grad (through x[row] and
+    # cat([x, s]), GNN.py:85-86,105-106) become the gin_* vectors
+    xg = x.clone().requires_grad_(True)
+    eag = ea.clone().requires_grad_(True)
+    pred = model(_Data(xg, ei, eag, batch))
     loss = torch.nn.MSELoss(reduction="sum")(pred, y.view_as(pred))
     loss.backward()
 
@@ -166,6 +171,8 @@ def run_case(ref, name, bkw, mkw, extra):
         out["p_" + k] = v.numpy()
     for k, p in model.named_parameters():
         out["g_" + k] = p.grad.numpy()
+    out["gin_x"] = xg.grad.numpy()
+    out["gin_edge_attr"] = (eag.grad if eag.grad is not None else torch.zeros_like(ea)).numpy()
     meta = dict(name=name, depth=D, hidden=H, act=mkw["act"], skip=mkw["skip"],
                 batch_none=bool(extra.get("batch_none")), eval_dropout=p_eval,
                 num_node_features=int(x.shape[1]), num_edge_features=int(ea.shape[1]),

@@ -105,6 +105,62 @@ def test_gradients_match_reference_golden(case, cuda_device):
         assert_g_close(p.grad.cpu().numpy(), z["g_" + k], k)
 
 
+@pytest.mark.parametrize("case", golden_cases())
+def test_input_gradients_match_reference_golden(case, cuda_device):
+    """x.grad / edge_attr.grad (cgr_gnn_input_grads) vs the reference's autograd (gin_*); the
+    parameter gradients of the same backward are bitwise those of a run without input grads."""
+    z, meta = load_golden(case)
+    m = model_from_golden(z, meta, cuda_device, dropout=0.0)
+    m.train()
+    data = batch_from_golden(z, meta, cuda_device)
+    data.x.requires_grad_(True)
+    data.edge_attr.requires_grad_(True)
+    pred = m(data)
+    torch.nn.MSELoss(reduction="sum")(pred, data.y.view_as(pred)).backward()
+    assert data.x.grad.shape == tuple(z["gin_x"].shape)
+    assert data.edge_attr.grad.shape == tuple(z["gin_edge_attr"].shape)
+    assert_g_close(data.x.grad.cpu().numpy(), z["gin_x"], "x")
+    if z["gin_edge_attr"].size:
+        assert_g_close(data.edge_attr.grad.cpu().numpy(), z["gin_edge_attr"], "edge_attr")
+    with_inputs = {k: p.grad.clone() for k, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    data2 = batch_from_golden(z, meta, cuda_device)
+    pred2 = m(data2)
+    torch.nn.MSELoss(reduction="sum")(pred2, data2.y.view_as(pred2)).backward()
+    for k, p in m.named_parameters():
+        assert torch.equal(p.grad, with_inputs[k]), k
+
+
+def test_input_gradients_only_x_and_frozen_parameters(cuda_device):
+    """Only x requires grad, every parameter frozen: the training forward still runs (not the
+    no-grad predict path) and edge_attr gets no gradient."""
+    z, meta = load_golden("ragged_gelu")
+    m = model_from_golden(z, meta, cuda_device, dropout=0.0)
+    m.train()
+    for p in m.parameters():
+        p.requires_grad_(False)
+    data = batch_from_golden(z, meta, cuda_device)
+    data.x.requires_grad_(True)
+    pred = m(data)
+    assert pred.requires_grad
+    torch.nn.MSELoss(reduction="sum")(pred, data.y.view_as(pred)).backward()
+    assert data.edge_attr.grad is None
+    assert_g_close(data.x.grad.cpu().numpy(), z["gin_x"], "x")
+    assert all(p.grad is None for p in m.parameters())
+
+
+def test_cfg2_input_gradients_vs_oracle(cuda_device):
+    # the real cfg2 widths on 32 reactions: F = 846 (x concat), H = 400
+    _oracle_compare(make_batch(32, seed=23), 400, 4, "relu", False, cuda_device, inputs=True)
+
+
+@pytest.mark.parametrize("H,act", [(21, "silu"), (18, "gelu"), (64, "relu")])
+def test_input_gradients_odd_widths_vs_oracle(H, act, cuda_device):
+    # H % 4 != 0: the [Gs | dzn] concat loader's narrower vector widths; x of F = 78 (padded rows)
+    b = make_batch(6, n_atoms=14, n_bonds=16, n_mace=0, seed=31, n_atoms_jitter=5)
+    _oracle_compare(b, H, 3, act, True, cuda_device, inputs=True)
+
+
 def _cfg_tuple(F_, Fe, H, D, act, skip):
     return (F_, Fe, H, D, {"relu": 0, "silu": 1, "gelu": 2}[act], skip)
 
@@ -182,7 +238,9 @@ def _write_report():
         pass
 
 
-def _oracle_compare(b, H, D, act, skip, dev, seed=0, case=None):
+def _oracle_compare(b, H, D, act, skip, dev, seed=0, case=None, inputs=False):
+    """inputs: x / edge_attr require grad; their gradients are checked against the oracle too
+    (the parameter gradients are the same computation either way)."""
     F_, Fe = b.x.shape[1], b.edge_attr.shape[1]
     torch.manual_seed(seed)
     m = GNN(F_, Fe, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D, activation_fn=ACT[act],
@@ -194,18 +252,27 @@ def _oracle_compare(b, H, D, act, skip, dev, seed=0, case=None):
     sd = {k: v.detach().numpy().copy() for k, v in m.state_dict().items()}
     m = m.to(dev).train()
     data = b.to_torch(dev)
+    if inputs:
+        data.x.requires_grad_(True)
+        data.edge_attr.requires_grad_(True)
     pred = m(data)
     loss = torch.nn.MSELoss(reduction="sum")(pred, data.y)
     loss.backward()
     oc = {}
+    gin_o = {} if inputs else None
     loss_o, y_o, g_o = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, D, act,
-                                         skip, num_graphs=b.num_graphs, cache_out=oc)
+                                         skip, num_graphs=b.num_graphs, cache_out=oc,
+                                         inputs_out=gin_o)
     assert_y_close(pred.detach().cpu().numpy(), y_o)
     grads = {k: p.grad.cpu().numpy() for k, p in m.named_parameters()}
+    if inputs:
+        grads["input:x"] = data.x.grad.cpu().numpy()
+        grads["input:edge_attr"] = data.edge_attr.grad.cpu().numpy()
+        g_o = dict(g_o, **{"input:" + k: v for k, v in gin_o.items()})
     skip_abs = oc.get("skip_abs", {})
     flips = 0
     if act == "relu" and not all(_g_ok(grads[k], g_o[k], skip_abs.get(k)) for k in grads):
-        g_o, flips = _reconciled_relu_grads(m, data, b, sd, D, skip, grads)
+        g_o, flips = _reconciled_relu_grads(m, data, b, sd, D, skip, grads, inputs)
     if case is not None:
         E = b.edge_index.shape[1]
         RECONCILIATIONS[case] = {"relu_decisions_from_gpu": int(flips),
@@ -227,7 +294,7 @@ def _g_ok(g, ref, abs_sum=None):
 AMBIGUOUS_Z = 1e-5  # |z| <= AMBIGUOUS_Z * max|z| of its tensor: sign within fp32 rounding reach
 
 
-def _reconciled_relu_grads(m, data, b, sd, D, skip, grads):
+def _reconciled_relu_grads(m, data, b, sd, D, skip, grads, inputs=False):
     """Oracle gradients with the GPU's ReLU decisions at numerically ambiguous pre-activations.
 
     A pre-activation within rounding distance of 0 has no well-defined fp32 sign: any fp32
@@ -240,8 +307,8 @@ def _reconciled_relu_grads(m, data, b, sd, D, skip, grads):
     """
     F_, Fe = b.x.shape[1], b.edge_attr.shape[1]
     H = m.hidden_sizes[0]
-    run = ArenaRun(_cfg_tuple(F_, Fe, H, D, "relu", skip), data.x, data.edge_index,
-                   data.edge_attr, data.batch, data.ptr, b.num_graphs,
+    run = ArenaRun(_cfg_tuple(F_, Fe, H, D, "relu", skip), data.x.detach(), data.edge_index,
+                   data.edge_attr.detach(), data.batch, data.ptr, b.num_graphs,
                    [p.detach() for p in m.native_parameters()])
     torch.cuda.synchronize()
     N, E = b.x.shape[0], b.edge_index.shape[1]
@@ -272,8 +339,11 @@ def _reconciled_relu_grads(m, data, b, sd, D, skip, grads):
              "zs": [reconcile(cache["zs"][l], gpu["zs"][l], f"z{l + 1}") for l in range(D)],
              "zn": reconcile(cache["zn"], gpu["zn"], "zn")}
     assert flips > 0, "gradient mismatch with no ambiguous ReLU decision to explain it"
+    gin = {} if inputs else None
     _, _, g_o = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, D, "relu",
-                                  skip, num_graphs=b.num_graphs, relu_masks=masks)
+                                  skip, num_graphs=b.num_graphs, relu_masks=masks, inputs_out=gin)
+    if inputs:
+        g_o = dict(g_o, **{"input:" + k: v for k, v in gin.items()})
     return g_o, flips
 
 

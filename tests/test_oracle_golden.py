@@ -51,6 +51,22 @@ def test_numpy_oracle_gradients_match_reference(case):
 
 
 @pytest.mark.parametrize("case", CASES)
+def test_numpy_oracle_input_gradients_match_reference(case):
+    """x.grad / edge_attr.grad of the reference's autograd (gin_*, make_golden.py)."""
+    z, meta = load_golden(case)
+    params, batch = _inputs(z, meta)
+    gin = {}
+    on.loss_and_grads(params, z["in_x"], z["in_edge_index"], z["in_edge_attr"], batch,
+                      z["in_y"], meta["depth"], meta["act"], meta["skip"],
+                      num_graphs=len(z["in_ptr"]) - 1, inputs_out=gin)
+    assert gin["x"].shape == z["gin_x"].shape
+    assert gin["edge_attr"].shape == z["gin_edge_attr"].shape
+    assert rel_err(gin["x"], z["gin_x"]) < 1e-5
+    if z["gin_edge_attr"].size:
+        assert rel_err(gin["edge_attr"], z["gin_edge_attr"]) < 1e-5
+
+
+@pytest.mark.parametrize("case", CASES)
 def test_torch_restatement_is_bitwise_reference(case):
     z, meta = load_golden(case)
     params, batch = _inputs(z, meta)
