@@ -43,13 +43,18 @@ def test_dropout_masks_follow_manual_seed(cuda_device):
     assert not torch.equal(ys[0], ys[2])
 
 
-def test_input_gradients_rejected(cuda_device):
+def test_input_gradients_under_dropout_and_no_grad(cuda_device):
+    """x.grad through cgr_gnn_input_grads in train mode with dropout (the recorded mask applies to
+    both backward passes); no_grad still takes the forward-only path."""
     b = make_batch(4, n_mace=16, seed=5)
     data = b.to_torch(cuda_device)
-    m = _model(b.x.shape[1], cuda_device, p=0.0)
+    m = _model(b.x.shape[1], cuda_device, p=0.1)
+    m.train()
     data.x.requires_grad_(True)
-    with pytest.raises(NotImplementedError):
-        m(data)
+    y = m(data)
+    y.sum().backward()
+    assert data.x.grad is not None and torch.isfinite(data.x.grad).all()
+    assert data.x.grad.abs().sum() > 0
     with torch.no_grad():
         assert torch.isfinite(m(data)).all()
 

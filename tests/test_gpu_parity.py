@@ -161,6 +161,17 @@ def test_input_gradients_odd_widths_vs_oracle(H, act, cuda_device):
     _oracle_compare(b, H, 3, act, True, cuda_device, inputs=True)
 
 
+@pytest.mark.parametrize("Fe", [3, 5, 9, 14])
+def test_edge_feature_widths_vs_oracle(Fe, cuda_device):
+    """The edge-feature weight gradient dW0[:, F:] = dpre0^T e (the side stream's fp32 TN) and
+    the edge_attr input gradient at several bond-feature widths (padded rows Fep = 4 .. 16)."""
+    import dataclasses
+
+    b = make_batch(24, n_mace=32, seed=41, n_atoms_jitter=6)
+    b = dataclasses.replace(b, edge_attr=np.ascontiguousarray(b.edge_attr[:, :Fe]))
+    _oracle_compare(b, 80, 3, "relu", False, cuda_device, inputs=True)
+
+
 def _cfg_tuple(F_, Fe, H, D, act, skip):
     return (F_, Fe, H, D, {"relu": 0, "silu": 1, "gelu": 2}[act], skip)
 
