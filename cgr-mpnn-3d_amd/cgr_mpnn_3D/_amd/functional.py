@@ -17,9 +17,11 @@ from . import config as _config
 from . import native
 
 
-def make_config(num_node_features, num_edge_features, hidden, depth, act_code, learnable_skip):
+def make_config(num_node_features, num_edge_features, hidden, depth, act_code, learnable_skip,
+                aggregation=0, pooling=0):
     return native.CgrGnnConfig(int(num_node_features), int(num_edge_features), int(hidden),
-                               int(depth), int(act_code), 1 if learnable_skip else 0)
+                               int(depth), int(act_code), 1 if learnable_skip else 0,
+                               int(aggregation), int(pooling))
 
 
 def _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, num_graphs):

@@ -29,6 +29,8 @@ class CgrGnnConfig(ctypes.Structure):
         ("depth", c_int32),
         ("activation", c_int32),
         ("learnable_skip", c_int32),
+        ("aggregation", c_int32),
+        ("pooling", c_int32),
     ]
 
 

@@ -1,6 +1,7 @@
 """Pooling functions accepted as ``GNN(pooling_fn=...)`` (the reference default is PyG's
-``global_add_pool``, ``GNN.py:5,23,110``).  The native path fuses add-pooling with the ffn head, so
-``pooling_fn`` is only inspected to select that fused head; these functions also work standalone.
+``global_add_pool``, ``GNN.py:5,23,110``; PyG's ``global_mean_pool`` is the other one the native
+head implements).  The native path fuses pooling with the ffn head, so ``pooling_fn`` is only
+inspected to select that fused head; these functions also work standalone.
 """
 
 from __future__ import annotations
@@ -18,6 +19,45 @@ def global_add_pool(x: torch.Tensor, batch: torch.Tensor | None, size: int | Non
     return out.index_add_(0, batch, x)
 
 
+def global_mean_pool(x: torch.Tensor, batch: torch.Tensor | None, size: int | None = None):
+    """Mean of node rows per graph id (PyG semantics: sum / max(count, 1); ``batch=None`` ->
+    ``x.mean(-2, keepdim)``)."""
+    if batch is None:
+        return x.mean(dim=-2, keepdim=x.dim() == 2)
+    if size is None:
+        size = int(batch.max()) + 1 if batch.numel() else 0
+    out = global_add_pool(x, batch, size)
+    cnt = torch.bincount(batch, minlength=size).clamp(min=1).to(x.dtype)
+    return out / cnt.view(-1, *([1] * (x.dim() - 1)))
+
+
 def is_add_pool(fn) -> bool:
     """True for this module's global_add_pool or PyG's (matched by name, PyG may be absent)."""
     return fn is global_add_pool or getattr(fn, "__name__", "") == "global_add_pool"
+
+
+def is_mean_pool(fn) -> bool:
+    """True for this module's global_mean_pool or PyG's (matched by name)."""
+    return fn is global_mean_pool or getattr(fn, "__name__", "") == "global_mean_pool"
+
+
+def pooling_code(fn) -> int:
+    """The native head's pooling (include/cgr_mpnn3d.h enum cgr_pooling) for ``pooling_fn``."""
+    if is_add_pool(fn):
+        return 0
+    if is_mean_pool(fn):
+        return 1
+    raise NotImplementedError(
+        f"cgr_mpnn_3D (MI355X): pooling_fn {getattr(fn, '__name__', fn)!r} has no native head; "
+        "supported are global_add_pool (the reference default) and global_mean_pool")
+
+
+def aggregation_code(aggr) -> int:
+    """PyG MessagePassing aggr -> include/cgr_mpnn3d.h enum cgr_aggregation."""
+    if aggr in ("add", "sum"):
+        return 0
+    if aggr == "mean":
+        return 1
+    raise NotImplementedError(
+        f"cgr_mpnn_3D (MI355X): aggr={aggr!r}; the native D-MPNN implements 'add' (= 'sum', the "
+        "reference default) and 'mean'")

@@ -32,9 +32,9 @@ import torch.nn.functional as F
 from .._amd import config as _config
 from .._amd import native
 from .._amd.functional import gnn_forward, gnn_predict
-from .._amd.pool import global_add_pool, is_add_pool
+from .._amd.pool import aggregation_code, global_add_pool, global_mean_pool, pooling_code
 
-__all__ = ["GNN", "DMPNNConv", "global_add_pool"]
+__all__ = ["GNN", "DMPNNConv", "global_add_pool", "global_mean_pool"]
 
 
 def _activation_code(fn) -> int:
@@ -177,14 +177,11 @@ class GNN(nn.Module):
             raise RuntimeError(
                 "cgr_mpnn_3D (MI355X) runs on the GPU only: move the model and the batch to "
                 "'cuda' (there is no CPU fallback)")
-        if not is_add_pool(self.pooling_fn):
-            raise NotImplementedError(
-                "cgr_mpnn_3D (MI355X): only global_add_pool is fused into the native head")
-        for conv in self.convs:
-            if conv.aggr != "add":
-                raise NotImplementedError(
-                    f"cgr_mpnn_3D (MI355X): aggr={conv.aggr!r}; the native D-MPNN implements "
-                    "aggr='add' (the reference default)")
+        pool = pooling_code(self.pooling_fn)
+        aggrs = {aggregation_code(conv.aggr) for conv in self.convs}
+        if len(aggrs) != 1:
+            raise NotImplementedError("cgr_mpnn_3D (MI355X): one aggr for every DMPNNConv")
+        aggr = aggrs.pop()
         act = _activation_code(self.activation_fn)
         H = self._uniform_hidden()
         drop = [float(self.dropout_ps[l]) for l in range(self.depth)]  # IndexError like GNN.py:101
@@ -246,7 +243,7 @@ class GNN(nn.Module):
         counter = self._cgr_rng_counter
         if counter.device != dev:
             counter = self._cgr_rng_counter = counter.to(dev)
-        cfg = (F_, Fe, H, self.depth, act, self.use_learnable_skip)
+        cfg = (F_, Fe, H, self.depth, act, self.use_learnable_skip, aggr, pool)
         params = [p.contiguous() for p in params]
         want_grad = any(p.requires_grad for p in params) or x.requires_grad or \
             edge_attr.requires_grad

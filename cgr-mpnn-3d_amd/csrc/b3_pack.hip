@@ -267,7 +267,8 @@ __device__ __forceinline__ void b3_tile_put(float (&tile)[32][kImgCols + 1], int
 __global__ __launch_bounds__(256) void k_readout_bwd_img(
     const float* __restrict__ dy, const float* __restrict__ wf, const int* __restrict__ node_graph,
     const float* __restrict__ hn, const float* __restrict__ zn, int64_t N, int H, int Hp, int act,
-    float* __restrict__ dzn, int colblocks, int cimg, b3_u4* __restrict__ img) {
+    float* __restrict__ dzn, int colblocks, int cimg, b3_u4* __restrict__ img,
+    const float* __restrict__ gscale) {
   __shared__ float tile[32][kImgCols + 1];
   const int64_t s = blockIdx.x / colblocks;
   const int c0 = (int)(blockIdx.x - s * colblocks) * kImgCols;
@@ -278,7 +279,8 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
     float4 o = f4zero();
     if (v < N && n < Hp) {
       const int64_t off = v * Hp + n;
-      const float d = dy[node_graph[v]];
+      const int gv = node_graph[v];
+      const float d = gscale ? dy[gv] * gscale[gv] : dy[gv];
       o.x = d * wf[min(n, H - 1)];
       o.y = d * wf[min(n + 1, H - 1)];
       o.z = d * wf[min(n + 2, H - 1)];
@@ -307,13 +309,13 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
 
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
-                           float* dzn, void* img, hipStream_t st) {
+                           float* dzn, void* img, hipStream_t st, const float* gscale) {
   if (N <= 0 || (!dzn && !img)) return hipSuccess;
   const int colblocks = (int)cdiv(Hp, kImgCols);
   const int64_t blocks = cdiv(N, 32) * colblocks;
   hipLaunchKernelGGL(k_readout_bwd_img, dim3((unsigned)blocks), dim3(256), 0, st, dy, wf,
                      node_graph, hn, zn, N, H, Hp, act, dzn, colblocks, b3_eimg_cols(H),
-                     static_cast<b3_u4*>(img));
+                     static_cast<b3_u4*>(img), gscale);
   return hipGetLastError();
 }
 

@@ -59,6 +59,8 @@ Dims make_dims(const cgr_gnn_config* cfg, int64_t N, int64_t E, int64_t B) {
   d.D = cfg->depth;
   d.act = cfg->activation;
   d.learnable_skip = cfg->learnable_skip ? 1 : 0;
+  d.aggr = cfg->aggregation;
+  d.pool = cfg->pooling;
   return d;
 }
 
@@ -113,6 +115,8 @@ static void layout_prefix(const Dims& d, ArenaLayout& L, Bump& b) {
   L.P = b.take(4 * N * Hp);
   L.Q = b.take(4 * N * Hp);
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
+  L.inv_deg = d.aggr == CGR_AGGR_MEAN ? b.take(4 * N) : kNone;
+  L.inv_cnt = d.pool == CGR_POOL_MEAN ? b.take(4 * B) : kNone;
   // partial sums of the layer GEMMs' hub segments (over >= 3 row tiles), one slot pair per tile
   const size_t rt = (size_t)cdiv(d.E, b3nt_rows((int)d.E, d.H));
   L.fpart = b.take(4 * rt * 2 * 16 *
@@ -221,6 +225,8 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.P = (float*)at(arena, L.P);
   f.Q = (float*)at(arena, L.Q);
   f.xp = (float*)at(arena, L.xp);
+  f.inv_deg = (float*)at(arena, L.inv_deg);
+  f.inv_cnt = (float*)at(arena, L.inv_cnt);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     f.h[l] = (float*)at(arena, L.h[l]);
     f.a[l] = (float*)at(arena, L.a[l]);
@@ -323,6 +329,10 @@ static int validate_config(const cgr_gnn_config* c) {
   CGR_CHECK(c->hidden >= 1, "cgr: hidden size must be >= 1");
   CGR_CHECK(c->depth >= 1 && c->depth <= CGR_MAX_DEPTH, "cgr: depth must be in [1, 32]");
   CGR_CHECK(c->activation >= 0 && c->activation <= 2, "cgr: unknown activation code");
+  CGR_CHECK(c->aggregation == CGR_AGGR_ADD || c->aggregation == CGR_AGGR_MEAN,
+            "cgr: unknown aggregation (CGR_AGGR_ADD, CGR_AGGR_MEAN)");
+  CGR_CHECK(c->pooling == CGR_POOL_ADD || c->pooling == CGR_POOL_MEAN,
+            "cgr: unknown pooling (CGR_POOL_ADD, CGR_POOL_MEAN)");
   return 0;
 }
 

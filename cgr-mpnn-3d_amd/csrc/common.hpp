@@ -96,6 +96,9 @@ __device__ __forceinline__ float4 f4sub(float4 a, float4 b) {
 __device__ __forceinline__ float4 f4add(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
+__device__ __forceinline__ float4 f4scale(float4 a, float s) {
+  return make_float4(a.x * s, a.y * s, a.z * s, a.w * s);
+}
 
 // Load 4 consecutive floats p[0..3] of a row whose valid length from p is `valid` (elements at
 // index >= valid read as 0).  VEC = guaranteed alignment/divisibility of the row and of the

@@ -79,6 +79,8 @@ struct EpLayerBwdSeg {
   int* gcnt;           // unpaired form: this launch's grid ticket counter (zero on entry)
   int* dev_err;        // host-visible error words (kDevErr*), or null
   int spin_limit;      // unpaired completers' wait bound (< 0: report at once; debug knob)
+  // mean aggregation: a = segsum_dst(h) / deg, so dh gets da[dst] / deg(dst) (nullable: add)
+  const float* dscale;
 
   struct Ctx {};
   __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
@@ -154,6 +156,7 @@ struct EpLayerBwdSeg {
             }
           }
         } else {
+          if (dscale) da = f4scale(da, dscale[v]);
           bwd_row_apply<EDGE_INIT, A>(a, i, col, f4sub(da, x), key, dsig, pv[it]);
         }
       }
@@ -230,7 +233,7 @@ struct EpLayerBwdSeg {
                 da = f4add(da, sc1_load4(part + ((int64_t)(t * tiles_n + tn) * 2 + slot_of(t, t0)) *
                                                     BN + 4 * c4));
             }
-            das[c4] = da;
+            das[c4] = dscale ? f4scale(da, dscale[v]) : da;
           }
           __syncthreads();
           for (int q = tid; q < (ie - ib) * C4; q += NT) {
@@ -283,6 +286,7 @@ struct EpLayerBwdSeg {
           float4 da = make_float4(poison, poison, poison, poison);
           for (int j = src_ptr[v], e = src_ptr[v + 1]; j < e; ++j)
             da = f4add(da, sc1_load4(raw + (int64_t)a.rev_s[src_list[j]] * a.Hp + col));
+          if (dscale) da = f4scale(da, dscale[v]);
           for (int i = dst_ptr[v], e = dst_ptr[v + 1]; i < e; ++i) {
             const float4 x = sc1_load4(raw + (int64_t)i * a.Hp + col);
             bwd_row_apply<EDGE_INIT>(a, i, col, f4sub(da, x), key, ds,

@@ -92,6 +92,8 @@ struct EpStorePermRows {
 
 // C[r, :] = s_r * acc with s_r = dy[node_graph[r]] (readout backward ds = dzn W_n[:, F:], the
 // row factor of dzn; LdActGrad).  Internal [M, ld] buffers, ld % 4 == 0.
+// gscale / nscale (nullable): mean pooling's per-graph 1 / count, mean aggregation's per-node
+// 1 / in-degree (ds feeds dh_D = ds[dst] / deg(dst) only)
 struct EpStoreRowScale {
   static constexpr bool kSeg = false;
   float* C;
@@ -99,11 +101,20 @@ struct EpStoreRowScale {
   int M, N;
   const float* dy;
   const int* node_graph;
+  const float* gscale = nullptr;
+  const float* nscale = nullptr;
   struct Ctx {};
   __device__ __forceinline__ Ctx ctx(int) const { return Ctx{}; }
   __device__ __forceinline__ void finish_ctx(Ctx&) const {}
   typedef float Pre;
-  __device__ __forceinline__ Pre pre4(int r, int) const { return dy[node_graph[min(r, M - 1)]]; }
+  __device__ __forceinline__ Pre pre4(int r, int) const {
+    const int rr = min(r, M - 1);
+    const int g = node_graph[rr];
+    float s = dy[g];
+    if (gscale) s *= gscale[g];
+    if (nscale) s *= nscale[rr];
+    return s;
+  }
   __device__ __forceinline__ void apply4p(int r, int c, float4 v, Pre s, const Ctx&) const {
     if (r >= M || c >= N) return;
     *reinterpret_cast<float4*>(C + (int64_t)r * ld + c) =

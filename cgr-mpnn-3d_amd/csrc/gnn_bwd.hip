@@ -215,7 +215,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       ProfScope _p("readout_act_bwd", side);
       HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
                               Hp, d.act, ro_b3 ? nullptr : dzn, ro_b3 ? img_side : nullptr,
-                              side));
+                              side, fv.inv_cnt));
     }
     TnPlan p;
     float* sl = slabs[sb];
@@ -283,7 +283,8 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     ProfScope _p("gemm_nt_readout_bwd", st);
     const float* m = d.act == ACT_RELU ? fv.hn : fv.zn;
     const b3_u4* img = static_cast<const b3_u4*>(fv.b3rob);
-    const EpStoreRowScale ep{ds, Hp, N, H, dy, iv.node_graph};
+    // (mean pooling: dy / graph count; mean aggregation: ds / in-degree, for dh_D = ds[dst])
+    const EpStoreRowScale ep{ds, Hp, N, H, dy, iv.node_graph, fv.inv_cnt, fv.inv_deg};
     const B3Cols rc = b3nt_cols(N, H);  // the image's tiling (gnn_fwd.hip)
     // the activation derivative in the A loader, specialised per activation (main-loop code)
     if (d.act == ACT_RELU)
@@ -397,13 +398,13 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         HIP_RET(launch_b3nt(al, img, lcols,
                             EpLayerBwdSeg<false>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
                                                  iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
-                                                 seg_cols, gcnt, ss->dev_err, spin},
+                                                 seg_cols, gcnt, ss->dev_err, spin, fv.inv_deg},
                             E, H, H, st));
       else
         HIP_RET(launch_b3nt(al, img, lcols,
                             EpLayerBwdSeg<true>{lb, dm, iv.dst_s, iv.dst_ptr, iv.src_list,
                                                 iv.src_ptr, dg, dgn, part, cnt, iv.status, E, H, N,
-                                                seg_cols, gcnt, ss->dev_err, spin},
+                                                seg_cols, gcnt, ss->dev_err, spin, fv.inv_deg},
                             E, H, H, st));
     }
     if (fork_ev) HIP_RET(hipStreamWaitEvent(side, fork_ev, 0));
@@ -573,7 +574,7 @@ int gnn_input_grads_impl(const Dims& d, const float* const* params, const void* 
       ProfScope _p("input_grad_prep", st);
       HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, H, Gs, Hp, st));
       HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
-                              Hp, d.act, dzn, nullptr, st));
+                              Hp, d.act, dzn, nullptr, st, fv.inv_cnt));
       TransposeJobs tj{};  // wxT [F, ldw] = [W0[:, :F]^T | W_n[:, :F]^T]
       tj.job[0] = TransposeJob{params[CGR_PARAM_EDGE_INIT_W], F + Fe, 0, wxT, ldw, H, F};
       tj.job[1] = TransposeJob{params[CGR_PARAM_E2N_W(D)], F + H, 0, wxT + H, ldw, H, F};

@@ -258,6 +258,20 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     if (p_ready) HIP_RET(hipStreamWaitEvent(st, p_ready, 0));
   }
 
+  // mean aggregation / pooling (DMPNNConv(aggr="mean"), global_mean_pool): the per-node and
+  // per-graph factors once the CSRs exist; every a_l is formed as the sum and scaled in place
+  // right after the launch that completes it (scale_rows), before anything reads it
+  if (fv.inv_deg || fv.inv_cnt) {
+    ProfScope _p("mean_scales", st);
+    HIP_RET(mean_scales(iv.dst_ptr, N, iv.graph_ptr, d.B, fv.inv_deg, fv.inv_cnt, st));
+  }
+  auto mean_of = [&](float* a) -> int {
+    if (!fv.inv_deg) return 0;
+    ProfScope _p("mean_aggr", st);
+    HIP_RET(scale_rows(a, Hp, N, fv.inv_deg, st));
+    return 0;
+  };
+
   // the layer GEMMs sum their dst segments in the epilogue (EpLayerSeg: one gather -> MLP ->
   // segmented-reduce launch per layer) when the fused edge init zeroes what they accumulate
   const bool fused_seg = Hp <= 512;
@@ -280,6 +294,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
     ProfScope _p("segsum_dst_fwd", st);
     HIP_RET(segment_sum(fv.h[0], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[0], Hp, st));
   }
+  if (const int rc = mean_of(fv.a[0])) return rc;
 
   for (int l = 0; l < D; ++l) {
     uint32_t thresh;
@@ -312,6 +327,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
       ProfScope _p2("segsum_dst_fwd", st);
       HIP_RET(segment_sum(fv.h[l + 1], Hp, nullptr, iv.dst_ptr, N, Hp, fv.a[l + 1], Hp, st));
     }
+    if (const int rc = mean_of(fv.a[l + 1])) return rc;
   }
 
   // readout: hn = act(s W_n[:, F:]^T + Q + b_n), s = a_D
@@ -323,7 +339,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
   ProfScope _p("pool_head_fwd", st);
   HIP_RET(pool_head_fwd(fv.hn, Hp, iv.graph_ptr, d.B, H, params[CGR_PARAM_FFN_W(D)],
-                        params[CGR_PARAM_FFN_B(D)], fv.g, y, st));
+                        params[CGR_PARAM_FFN_B(D)], fv.g, y, st, fv.inv_cnt));
   return 0;
 }
 

@@ -80,6 +80,8 @@ struct FloatView {
   float* zn;                      // [N, Hp] readout pre-activation (non-ReLU only)
   float* hn;                      // [N, Hp] readout activation
   float* g;                       // [B, Hp] pooled graph embeddings
+  float* inv_deg;  // [N] 1 / max(in-degree, 1)   (mean aggregation; else nullptr)
+  float* inv_cnt;  // [B] 1 / max(graph nodes, 1) (mean pooling; else nullptr)
   // split-bf16 weight images (gemm_b3.hpp), packed once per step by the forward:
   void* b3x;                      // [W0[:, :F]; W_n[:, :F]]   (x-GEMM)
   void* b3rof;                    // W_n[:, F:]                 (readout forward)
@@ -93,6 +95,7 @@ struct Dims {
   int F, Fe, Fep, Fp, H, Hp, D;  // Fp = round_up(F, 4)
   int act;
   int learnable_skip;
+  int aggr, pool;  // enum cgr_aggregation / cgr_pooling
 };
 
 struct ArenaLayout {
@@ -105,6 +108,7 @@ struct ArenaLayout {
       node_graph;
   size_t e_s, w0eT, P, Q, xp, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1],
       pre[CGR_MAX_DEPTH + 1], zn, hn, g;
+  size_t inv_deg, inv_cnt;  // mean aggregation / pooling: 1 / max(count, 1) per node / graph
   size_t b3x, b3rof, b3rob, b3lf[CGR_MAX_DEPTH], b3lb[CGR_MAX_DEPTH];
 };
 

@@ -341,10 +341,12 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
                                                             const float* __restrict__ wf,
                                                             const float* __restrict__ bf,
                                                             float* __restrict__ g,
-                                                            float* __restrict__ y) {
+                                                            float* __restrict__ y,
+                                                            const float* __restrict__ inv_cnt) {
   const int b = blockIdx.x;
   const int v0 = gptr[b], v1 = gptr[b + 1];
   const int C4 = Hp >> 2;
+  const float gs = inv_cnt ? inv_cnt[b] : 1.f;  // global_mean_pool: the sum / node count
   float dot = 0.f;
   for (int c = threadIdx.x; c < C4; c += kPoolThreads) {
     const float* col = hn + 4 * c;
@@ -359,6 +361,7 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
       for (int u = 0; u < kPoolBatch; ++u)
         if (v + u < v1) s = f4add(s, x[u]);
     }
+    if (inv_cnt) s = make_float4(s.x * gs, s.y * gs, s.z * gs, s.w * gs);
     *reinterpret_cast<float4*>(g + (int64_t)b * Hp + 4 * c) = s;
     const int n = 4 * c;
     const float sv[4] = {s.x, s.y, s.z, s.w};
@@ -379,10 +382,51 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
 }
 
 hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
-                         const float* wf, const float* bf, float* g, float* y, hipStream_t st) {
+                         const float* wf, const float* bf, float* g, float* y, hipStream_t st,
+                         const float* inv_cnt) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pool_head, dim3(B), dim3(kPoolThreads), 0, st, hn, Hp, gptr, H, wf, bf, g,
-                     y);
+                     y, inv_cnt);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------
+// mean aggregation / mean pooling (PyG scatter mean: sum / max(count, 1))
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_mean_scales(const int* __restrict__ dst_ptr, int64_t N,
+                                                     const int* __restrict__ gptr, int64_t B,
+                                                     float* __restrict__ inv_deg,
+                                                     float* __restrict__ inv_cnt) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (inv_deg && t < N) inv_deg[t] = 1.f / (float)max(dst_ptr[t + 1] - dst_ptr[t], 1);
+  if (inv_cnt && t < B) inv_cnt[t] = 1.f / (float)max(gptr[t + 1] - gptr[t], 1);
+}
+
+hipError_t mean_scales(const int* dst_ptr, int64_t N, const int* gptr, int64_t B, float* inv_deg,
+                       float* inv_cnt, hipStream_t st) {
+  const int64_t n = std::max(inv_deg ? N : 0, inv_cnt ? B : 0);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_mean_scales, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, st, dst_ptr, N,
+                     gptr, B, inv_deg, inv_cnt);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_scale_rows(float* __restrict__ a, int Hp, int64_t N,
+                                                    const float* __restrict__ s) {
+  const int C4 = Hp >> 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * C4) return;
+  const int64_t v = t / C4;
+  float4* p = reinterpret_cast<float4*>(a) + t;
+  const float4 x = *p;
+  const float f = s[v];
+  *p = make_float4(x.x * f, x.y * f, x.z * f, x.w * f);
+}
+
+hipError_t scale_rows(float* a, int Hp, int64_t N, const float* s, hipStream_t st) {
+  const int64_t tot = N * (Hp >> 2);
+  if (tot <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scale_rows, dim3((unsigned)cdiv(tot, 256)), dim3(256), 0, st, a, Hp, N, s);
   return hipGetLastError();
 }
 

@@ -52,7 +52,16 @@ typedef struct cgr_gnn_config {
   int32_t depth;             /* D  (1 .. CGR_MAX_DEPTH) */
   int32_t activation;        /* enum cgr_activation */
   int32_t learnable_skip;    /* use_learnable_skip (GNN.py:71-74, :94-97) */
+  int32_t aggregation;       /* enum cgr_aggregation: DMPNNConv(aggr=...) (GNN.py:22,63,119) */
+  int32_t pooling;           /* enum cgr_pooling: pooling_fn (GNN.py:23,110) */
 } cgr_gnn_config;
+
+/* aggr of GNN.__init__ / DMPNNConv (PyG MessagePassing): "add" (= "sum", the default) or "mean"
+ * (the sum over a node's in-edges divided by their count, 0 for a node without in-edges) */
+enum cgr_aggregation { CGR_AGGR_ADD = 0, CGR_AGGR_MEAN = 1 };
+/* pooling_fn: global_add_pool (default) or global_mean_pool (the graph's node sum divided by its
+ * node count) */
+enum cgr_pooling { CGR_POOL_ADD = 0, CGR_POOL_MEAN = 1 };
 
 /* One collated batch, the fields GNN.forward reads from a PyG Batch (GNN.py:77-82). */
 typedef struct cgr_batch {

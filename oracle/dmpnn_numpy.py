@@ -116,8 +116,13 @@ def _scatter_sum(vals: np.ndarray, index: np.ndarray, n: int) -> np.ndarray:
 def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str = "relu",
             learnable_skip: bool = False, num_graphs: int | None = None,
             dropout_masks: list | None = None, dropout_ps: list | None = None,
-            relu_masks: dict | None = None):
+            relu_masks: dict | None = None, aggr: str = "add", pool: str = "add"):
     """GNN.forward (GNN.py:76-110) in float64. Returns (y[B], cache).
+
+    ``aggr`` ("add" / "mean"): DMPNNConv's PyG aggregation (GNN.py:22,63,119); ``pool`` ("add" /
+    "mean"): global_add_pool / global_mean_pool (GNN.py:23,110).  PyG's mean is the sum divided
+    by max(count, 1) (torch_geometric.utils.scatter, reduce="mean"; PyG is absent here, its
+    semantics restated).
 
     ``params`` uses the reference ``state_dict`` keys.  ``dropout_masks[l]`` (optional, 0/1 per
     element of h) + ``dropout_ps[l]`` reproduce ``F.dropout`` in train mode with a given mask.
@@ -138,6 +143,10 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     sig = [float(np.asarray(params[f"skip_weights.{l}"])) if learnable_skip else 1.0
            for l in range(depth)]
     rev = np.arange(E) ^ 1
+    assert aggr in ("add", "sum", "mean") and pool in ("add", "mean")
+    inv_deg = np.ones(N)
+    if aggr == "mean":
+        inv_deg = 1.0 / np.maximum(np.bincount(dst, minlength=N)[:N], 1)
 
     # GNN.py:85-87  h0 = act(edge_init(cat[x[row], edge_attr]))
     rm = relu_masks if (relu_masks is not None and act == "relu") else None
@@ -156,7 +165,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     for l in range(depth):
         Wl = np.asarray(params[f"convs.{l}.lin.weight"], f8)
         bl = np.asarray(params[f"convs.{l}.lin.bias"], f8)
-        a = _scatter_sum(h, dst, N)  # GNN.py:134 propagate (sum at edge_index[1])
+        a = _scatter_sum(h, dst, N) * inv_deg[:, None]  # GNN.py:134 propagate at edge_index[1]
         m = a[src] - h[rev]  # GNN.py:136-141
         z = m @ Wl.T + bl + sig[l] * h0  # GNN.py:141 + GNN.py:94-97
         hn = relu_or_mask(z, "zs", l)  # GNN.py:100-102
@@ -167,7 +176,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
         zs.append(z)
         h = hn
         hs.append(h)
-    s = _scatter_sum(h, dst, N)  # GNN.py:105 (readout aggregate; dead lin output dropped)
+    s = _scatter_sum(h, dst, N) * inv_deg[:, None]  # GNN.py:105 (dead lin output dropped)
     Wn = np.asarray(params["edge_to_node.weight"], f8)
     bn = np.asarray(params["edge_to_node.bias"], f8)
     qn = np.concatenate([x, s], axis=1)  # GNN.py:106
@@ -181,13 +190,18 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
         gid = np.asarray(batch, dtype=np.int64)
         B = int(num_graphs if num_graphs is not None else gid.max() + 1)
         g = _scatter_sum(hnode, gid, B)  # GNN.py:110 global_add_pool
+    inv_cnt = np.ones(B)
+    if pool == "mean":  # global_mean_pool
+        inv_cnt = 1.0 / np.maximum(np.bincount(gid, minlength=B)[:B], 1)
+        g = g * inv_cnt[:, None]
     wf = np.asarray(params["ffn.weight"], f8)  # [1, H]
     bf = np.asarray(params["ffn.bias"], f8)
     y = (g @ wf.T + bf)[:, 0]
     cache = dict(x=x, ea=ea, src=src, dst=dst, rev=rev, q0=q0, z0=z0, hs=hs, As=As, ms=ms,
                  zs=zs, s=s, qn=qn, zn=zn, hnode=hnode, g=g, gid=gid, B=B, sig=sig, N=N, E=E,
                  depth=depth, act=act, learnable_skip=learnable_skip,
-                 masks=dropout_masks, ps=dropout_ps, relu_masks=rm)
+                 masks=dropout_masks, ps=dropout_ps, relu_masks=rm, inv_deg=inv_deg,
+                 inv_cnt=inv_cnt)
     return y, cache
 
 
@@ -214,14 +228,15 @@ def backward(params: dict, cache: dict, dy: np.ndarray, inputs_out: dict | None 
         mk = rm[key] if l is None else rm[key][l]
         return mk.astype(z.dtype)
 
-    dhnode = dg[cache["gid"]]  # pooling backward = gather by graph id
+    inv_deg, inv_cnt = cache["inv_deg"], cache["inv_cnt"]
+    dhnode = (dg * inv_cnt[:, None])[cache["gid"]]  # pooling backward = gather by graph id
     dzn = dhnode * grad_of(cache["zn"], "zn")
     grads["edge_to_node.weight"] = dzn.T @ cache["qn"]
     grads["edge_to_node.bias"] = dzn.sum(0)
     Wn = np.asarray(params["edge_to_node.weight"], f8)
     F_ = cache["x"].shape[1]
     ds = dzn @ Wn[:, F_:]  # [N, H]
-    dh = ds[dst]  # readout aggregate backward: gather at dst
+    dh = (ds * inv_deg[:, None])[dst]  # readout aggregate backward: gather at dst
     dh0 = np.zeros_like(cache["hs"][0])
     for l in range(D - 1, -1, -1):
         z = cache["zs"][l]
@@ -239,7 +254,7 @@ def backward(params: dict, cache: dict, dy: np.ndarray, inputs_out: dict | None 
         dh0 += cache["sig"][l] * dz
         dm = dz @ Wl  # [E, H]
         da = _scatter_sum(dm, src, N)  # m = a[src] - h[rev]  ->  da = scatter_src(dm)
-        dh = da[dst] - dm[rev]  # a = scatter_dst(h) ; rev is an involution
+        dh = (da * inv_deg[:, None])[dst] - dm[rev]  # a = scatter_dst(h) ; rev: involution
     dh0 += dh
     dz0 = dh0 * grad_of(cache["z0"], "z0")
     grads["edge_init.weight"] = dz0.T @ cache["q0"]
@@ -255,12 +270,12 @@ def backward(params: dict, cache: dict, dy: np.ndarray, inputs_out: dict | None 
 
 def loss_and_grads(params, x, edge_index, edge_attr, batch, y_true, depth, act="relu",
                    learnable_skip=False, num_graphs=None, relu_masks=None, cache_out=None,
-                   inputs_out=None):
+                   inputs_out=None, aggr="add", pool="add"):
     """MSELoss(reduction='sum') (train.py:120) forward + backward: (loss, y_hat, grads).
     `cache_out` (a dict, optional) receives the forward / backward cache (incl. "skip_abs");
     `inputs_out` (a dict, optional) the input gradients (``backward``)."""
     y, cache = forward(params, x, edge_index, edge_attr, batch, depth, act, learnable_skip,
-                       num_graphs, relu_masks=relu_masks)
+                       num_graphs, relu_masks=relu_masks, aggr=aggr, pool=pool)
     r = y - np.asarray(y_true, np.float64)
     loss = float((r * r).sum())
     grads = backward(params, cache, 2.0 * r, inputs_out)

@@ -17,7 +17,7 @@ the train-mode (dropout p=0) ``MSELoss(sum)`` loss, every parameter gradient and
 with respect to ``x`` / ``edge_attr`` (``gin_*``).  Only these data
 files are committed; the reference itself never leaves this container.
 
-    python tests/golden/make_golden.py
+    python tests/golden/make_golden.py [case ...]
 """
 
 from __future__ import annotations
@@ -51,15 +51,23 @@ def _scatter_sum(src: torch.Tensor, index: torch.Tensor, dim_size: int | None) -
     return out.scatter_add_(0, idx, src)
 
 
+def _scatter_mean(src: torch.Tensor, index: torch.Tensor, dim_size: int | None) -> torch.Tensor:
+    # PyG utils.scatter(reduce="mean"): the sum divided by the count clamped to >= 1
+    out = _scatter_sum(src, index, dim_size)
+    cnt = torch.bincount(index, minlength=out.shape[0]).clamp(min=1).to(src.dtype)
+    return out / cnt.view(-1, *([1] * (src.dim() - 1)))
+
+
 class _MessagePassing(torch.nn.Module):
     def __init__(self, aggr: str = "add"):
         super().__init__()
-        assert aggr == "add", "stand-in restates sum aggregation only"
+        assert aggr in ("add", "sum", "mean"), "stand-in restates sum / mean aggregation only"
         self.aggr = aggr
 
     def propagate(self, edge_index, size=None, **kwargs):
         msg = self.message(kwargs["edge_attr"])
-        return _scatter_sum(msg, edge_index[1], None if size is None else size[1])
+        red = _scatter_mean if self.aggr == "mean" else _scatter_sum
+        return red(msg, edge_index[1], None if size is None else size[1])
 
 
 def _global_add_pool(x, batch, size=None):
@@ -68,11 +76,18 @@ def _global_add_pool(x, batch, size=None):
     return _scatter_sum(x, batch, size)
 
 
+def _global_mean_pool(x, batch, size=None):
+    if batch is None:
+        return x.mean(dim=-2, keepdim=x.dim() == 2)
+    return _scatter_mean(x, batch, size)
+
+
 def _install_pyg_standin():
     tg = types.ModuleType("torch_geometric")
     tgnn = types.ModuleType("torch_geometric.nn")
     tgnn.MessagePassing = _MessagePassing
     tgnn.global_add_pool = _global_add_pool
+    tgnn.global_mean_pool = _global_mean_pool
     tg.nn = tgnn
     sys.modules["torch_geometric"] = tg
     sys.modules["torch_geometric.nn"] = tgnn
@@ -120,6 +135,18 @@ CASES = {
     # denser, larger graphs (stress-shaped, small): 60 atoms / 120 bonds
     "dense_relu_skip": (dict(num_graphs=3, n_atoms=60, n_bonds=120, n_mace=64, seed=18),
                         dict(depth=4, hidden=80, act="relu", skip=True), {}),
+    # DMPNNConv(aggr="mean") (GNN.py:22,63,119), ragged graphs
+    "mean_aggr_relu": (dict(num_graphs=5, n_atoms=18, n_bonds=20, n_mace=16, seed=20,
+                            n_atoms_jitter=6),
+                       dict(depth=3, hidden=40, act="relu", skip=False), {"aggr": "mean"}),
+    # pooling_fn=global_mean_pool (GNN.py:23,110), learnable skip
+    "mean_pool_silu_skip": (dict(num_graphs=4, n_atoms=14, n_bonds=15, n_mace=8, seed=21,
+                                 n_atoms_jitter=5),
+                            dict(depth=2, hidden=36, act="silu", skip=True), {"pool": "mean"}),
+    # both, one reaction with batch=None (global_mean_pool(h, None) = mean over all nodes)
+    "mean_both_gelu_none": (dict(num_graphs=1, n_atoms=16, n_bonds=17, n_mace=0, seed=22),
+                            dict(depth=2, hidden=24, act="gelu", skip=False),
+                            {"aggr": "mean", "pool": "mean", "batch_none": True}),
 }
 
 
@@ -136,9 +163,14 @@ def run_case(ref, name, bkw, mkw, extra):
 
     torch.manual_seed(1000 + len(name))
     p_eval = extra.get("eval_dropout", 0.0)
+    kw = {}
+    if extra.get("aggr"):
+        kw["aggr"] = extra["aggr"]
+    if extra.get("pool") == "mean":
+        kw["pooling_fn"] = _global_mean_pool
     model = ref.GNN(x.shape[1], ea.shape[1], depth=D, hidden_sizes=[H] * D,
                     dropout_ps=[p_eval] * D, activation_fn=ACTS[mkw["act"]],
-                    use_learnable_skip=mkw["skip"])
+                    use_learnable_skip=mkw["skip"], **kw)
     if mkw["skip"]:
         with torch.no_grad():
             for i, w in enumerate(model.skip_weights):
@@ -174,6 +206,7 @@ def run_case(ref, name, bkw, mkw, extra):
     out["gin_x"] = xg.grad.numpy()
     out["gin_edge_attr"] = (eag.grad if eag.grad is not None else torch.zeros_like(ea)).numpy()
     meta = dict(name=name, depth=D, hidden=H, act=mkw["act"], skip=mkw["skip"],
+                aggr=extra.get("aggr", "add"), pool=extra.get("pool", "add"),
                 batch_none=bool(extra.get("batch_none")), eval_dropout=p_eval,
                 num_node_features=int(x.shape[1]), num_edge_features=int(ea.shape[1]),
                 generator="cgr_mpnn_3D._amd.synth.make_batch", batch_kwargs=bkw,
@@ -210,13 +243,16 @@ def isolated_last_node_case(ref):
     print("isolated_last_node: reference raised", err)
 
 
-def main():
+def main(names=None):
+    """names: the cases to (re)generate (default: all, plus isolated_last_node)."""
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = load_reference_gnn()
     for name, (bkw, mkw, extra) in CASES.items():
-        run_case(ref, name, bkw, mkw, extra)
-    isolated_last_node_case(ref)
+        if not names or name in names:
+            run_case(ref, name, bkw, mkw, extra)
+    if not names or "isolated_last_node" in names:
+        isolated_last_node_case(ref)
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1:])

@@ -61,11 +61,18 @@ def assert_g_close(g, ref, name="", abs_sum=None):
 SKIP_COND_U = 2.0 ** -20
 
 
+def _pool_fn(pool):
+    from cgr_mpnn_3D.models.GNN import global_add_pool, global_mean_pool
+
+    return global_mean_pool if pool == "mean" else global_add_pool
+
+
 def model_from_golden(z, meta, dev, dropout=None):
     D, H = meta["depth"], meta["hidden"]
     m = GNN(meta["num_node_features"], meta["num_edge_features"], depth=D, hidden_sizes=[H] * D,
             dropout_ps=[dropout if dropout is not None else meta["eval_dropout"]] * D,
-            activation_fn=ACT[meta["act"]], use_learnable_skip=meta["skip"])
+            activation_fn=ACT[meta["act"]], use_learnable_skip=meta["skip"],
+            aggr=meta.get("aggr", "add"), pooling_fn=_pool_fn(meta.get("pool", "add")))
     sd = {k[2:]: torch.from_numpy(np.array(z[k])) for k in z.files if k.startswith("p_")}
     m.load_state_dict(sd)
     return m.to(dev)
@@ -172,8 +179,9 @@ def test_edge_feature_widths_vs_oracle(Fe, cuda_device):
     _oracle_compare(b, 80, 3, "relu", False, cuda_device, inputs=True)
 
 
-def _cfg_tuple(F_, Fe, H, D, act, skip):
-    return (F_, Fe, H, D, {"relu": 0, "silu": 1, "gelu": 2}[act], skip)
+def _cfg_tuple(F_, Fe, H, D, act, skip, aggr="add", pool="add"):
+    return (F_, Fe, H, D, {"relu": 0, "silu": 1, "gelu": 2}[act], skip,
+            {"add": 0, "mean": 1}[aggr], {"add": 0, "mean": 1}[pool])
 
 
 def _graph_prep_check(b, dev, use_ptr=True, batch_none=False):
@@ -249,13 +257,16 @@ def _write_report():
         pass
 
 
-def _oracle_compare(b, H, D, act, skip, dev, seed=0, case=None, inputs=False):
+def _oracle_compare(b, H, D, act, skip, dev, seed=0, case=None, inputs=False, aggr="add",
+                    pool="add"):
     """inputs: x / edge_attr require grad; their gradients are checked against the oracle too
-    (the parameter gradients are the same computation either way)."""
+    (the parameter gradients are the same computation either way).  aggr / pool: DMPNNConv's
+    aggregation and the pooling_fn ("add" or "mean")."""
     F_, Fe = b.x.shape[1], b.edge_attr.shape[1]
     torch.manual_seed(seed)
     m = GNN(F_, Fe, depth=D, hidden_sizes=[H] * D, dropout_ps=[0.0] * D, activation_fn=ACT[act],
-            use_learnable_skip=skip)
+            use_learnable_skip=skip, aggr=aggr, pooling_fn=_pool_fn(pool))
+    m._cgr_modes = dict(aggr=aggr, pool=pool)
     if skip:
         with torch.no_grad():
             for i, w in enumerate(m.skip_weights):
@@ -273,7 +284,7 @@ def _oracle_compare(b, H, D, act, skip, dev, seed=0, case=None, inputs=False):
     gin_o = {} if inputs else None
     loss_o, y_o, g_o = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, D, act,
                                          skip, num_graphs=b.num_graphs, cache_out=oc,
-                                         inputs_out=gin_o)
+                                         inputs_out=gin_o, aggr=aggr, pool=pool)
     assert_y_close(pred.detach().cpu().numpy(), y_o)
     grads = {k: p.grad.cpu().numpy() for k, p in m.named_parameters()}
     if inputs:
@@ -318,9 +329,10 @@ def _reconciled_relu_grads(m, data, b, sd, D, skip, grads, inputs=False):
     """
     F_, Fe = b.x.shape[1], b.edge_attr.shape[1]
     H = m.hidden_sizes[0]
-    run = ArenaRun(_cfg_tuple(F_, Fe, H, D, "relu", skip), data.x.detach(), data.edge_index,
-                   data.edge_attr.detach(), data.batch, data.ptr, b.num_graphs,
-                   [p.detach() for p in m.native_parameters()])
+    modes = getattr(m, "_cgr_modes", dict(aggr="add", pool="add"))
+    run = ArenaRun(_cfg_tuple(F_, Fe, H, D, "relu", skip, modes["aggr"], modes["pool"]),
+                   data.x.detach(), data.edge_index, data.edge_attr.detach(), data.batch, data.ptr,
+                   b.num_graphs, [p.detach() for p in m.native_parameters()])
     torch.cuda.synchronize()
     N, E = b.x.shape[0], b.edge_index.shape[1]
     perm = run.ints("perm", E).long().cpu().numpy()
@@ -334,7 +346,7 @@ def _reconciled_relu_grads(m, data, b, sd, D, skip, grads, inputs=False):
            "zs": [unsort(run.floats("h", E, index=l + 1).cpu().numpy()) > 0 for l in range(D)],
            "zn": run.floats("hn", N).cpu().numpy() > 0}
     _, cache = on.forward(sd, b.x, b.edge_index, b.edge_attr, b.batch, D, "relu", skip,
-                          b.num_graphs)
+                          b.num_graphs, **modes)
     flips = 0
 
     def reconcile(z, g, name):
@@ -352,7 +364,8 @@ def _reconciled_relu_grads(m, data, b, sd, D, skip, grads, inputs=False):
     assert flips > 0, "gradient mismatch with no ambiguous ReLU decision to explain it"
     gin = {} if inputs else None
     _, _, g_o = on.loss_and_grads(sd, b.x, b.edge_index, b.edge_attr, b.batch, b.y, D, "relu",
-                                  skip, num_graphs=b.num_graphs, relu_masks=masks, inputs_out=gin)
+                                  skip, num_graphs=b.num_graphs, relu_masks=masks, inputs_out=gin,
+                                  **modes)
     if inputs:
         g_o = dict(g_o, **{"input:" + k: v for k, v in gin.items()})
     return g_o, flips
@@ -862,13 +875,13 @@ def _hub_batch(leaves, seed):
                     ptr=np.array(ptr, np.int64), y=y)
 
 
-def _assert_bitwise_reruns(b, H, D, skip, dev, runs=3):
+def _assert_bitwise_reruns(b, H, D, skip, dev, runs=3, aggr="add"):
     # hub segments over >= 3 row tiles are summed from data-determined slots in row-tile order
     # (handoff.hpp): the forward (training and predict paths) and every gradient must repeat bit
     # for bit, whichever workgroup happens to finish last
     torch.manual_seed(5)
     m = GNN(b.x.shape[1], b.edge_attr.shape[1], depth=D, hidden_sizes=[H] * D,
-            dropout_ps=[0.0] * D, use_learnable_skip=skip).to(dev).train()
+            dropout_ps=[0.0] * D, use_learnable_skip=skip, aggr=aggr).to(dev).train()
     data = b.to_torch(dev)
     y0, g0 = _run(m, data)
     with torch.no_grad():
@@ -987,3 +1000,54 @@ def test_unpaired_batch_after_paired_ones_warns_without_a_sync(cuda_device):
             torch.nn.MSELoss(reduction="sum")(m(d), d.y).backward()
             torch.cuda.synchronize()
     assert wc.count == 1
+
+
+# ---------------------------------------------------------------------------------------------
+# DMPNNConv(aggr="mean") and pooling_fn=global_mean_pool (GNN.py:22-23,63,110,119): the means
+# are the sums scaled by 1 / max(count, 1) (a_l in place after the launch that completes it, the
+# pooled g in the pool kernel; the backward scales da / ds / dy), every fused path exercised
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("aggr,pool,act,skip", [("mean", "add", "relu", False),
+                                                ("add", "mean", "silu", True),
+                                                ("mean", "mean", "gelu", False)])
+def test_mean_modes_cfg2_widths_vs_oracle(aggr, pool, act, skip, cuda_device):
+    _oracle_compare(make_batch(32, seed=24, n_atoms_jitter=8), 400, 4, act, skip, cuda_device,
+                    inputs=True, aggr=aggr, pool=pool)
+
+
+def test_mean_aggregation_hub_segments_vs_oracle(cuda_device):
+    # crossing segments (two tiles: atomics; >= 3: slots) completed with da / deg
+    b = _hub_batch([150, 3, 70, 300, 5], seed=43)
+    _oracle_compare(b, 64, 3, "relu", True, cuda_device, aggr="mean", pool="mean")
+    _assert_bitwise_reruns(b, 64, 3, True, cuda_device, aggr="mean")
+
+
+def test_mean_aggregation_unpaired_vs_oracle(cuda_device):
+    u = _shuffled_pairs(make_batch(8, n_atoms=30, n_bonds=30, n_mace=16, seed=33), seed=8)
+    assert _pair_status(u, cuda_device) == 4
+    _oracle_compare(u, 64, 3, "relu", True, cuda_device, aggr="mean")
+    torch.cuda.synchronize()
+    native.raise_device_errors(cuda_device)
+
+
+def test_mean_modes_isolated_nodes_and_predict_path(cuda_device):
+    # atoms without bonds: mean over no in-edges is 0 (PyG clamps the count to 1); the eval
+    # forward (cgr_gnn_predict, ring-buffered a_l) equals the training forward bit for bit
+    b = _sparse_batch(6, 40, seed=34)
+    _oracle_compare(b, 64, 3, "relu", False, cuda_device, aggr="mean", pool="mean")
+    torch.manual_seed(3)
+    m = GNN(b.x.shape[1], 14, depth=3, hidden_sizes=[64] * 3, dropout_ps=[0.0] * 3,
+            aggr="mean", pooling_fn=_pool_fn("mean")).to(cuda_device).train()
+    data = b.to_torch(cuda_device)
+    y_train = m(data).detach()
+    with torch.no_grad():
+        y_eval = m(data)
+    assert torch.equal(y_train, y_eval)
+
+
+def test_unsupported_aggregation_and_pooling_raise(cuda_device):
+    b = make_batch(2, n_mace=8, seed=35)
+    for kw in (dict(aggr="max"), dict(pooling_fn=lambda h, batch: h.max(0)[0])):
+        m = GNN(b.x.shape[1], 14, depth=1, hidden_sizes=[16], **kw).to(cuda_device)
+        with pytest.raises(NotImplementedError):
+            m(b.to_torch(cuda_device))

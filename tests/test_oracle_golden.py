@@ -19,6 +19,11 @@ def _inputs(z, meta):
     return params, batch
 
 
+def _modes(meta):
+    """DMPNNConv aggr / pooling_fn of the golden case (older cases: the reference defaults)."""
+    return dict(aggr=meta.get("aggr", "add"), pool=meta.get("pool", "add"))
+
+
 def rel_err(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
@@ -30,7 +35,8 @@ def test_numpy_oracle_forward_matches_reference(case):
     z, meta = load_golden(case)
     params, batch = _inputs(z, meta)
     y, _ = on.forward(params, z["in_x"], z["in_edge_index"], z["in_edge_attr"], batch,
-                      meta["depth"], meta["act"], meta["skip"], num_graphs=len(z["in_ptr"]) - 1)
+                      meta["depth"], meta["act"], meta["skip"], num_graphs=len(z["in_ptr"]) - 1,
+                      **_modes(meta))
     ref = z["out_y_eval"]
     assert y.shape == ref.shape
     np.testing.assert_allclose(y, ref, rtol=1e-5, atol=1e-5 * np.abs(ref).max())
@@ -42,7 +48,8 @@ def test_numpy_oracle_gradients_match_reference(case):
     params, batch = _inputs(z, meta)
     loss, y, grads = on.loss_and_grads(params, z["in_x"], z["in_edge_index"], z["in_edge_attr"],
                                        batch, z["in_y"], meta["depth"], meta["act"],
-                                       meta["skip"], num_graphs=len(z["in_ptr"]) - 1)
+                                       meta["skip"], num_graphs=len(z["in_ptr"]) - 1,
+                                       **_modes(meta))
     assert abs(loss - float(z["out_loss"])) <= 1e-5 * abs(float(z["out_loss"]))
     ref_keys = {k[2:] for k in z.files if k.startswith("g_")}
     assert set(grads) == ref_keys
@@ -58,7 +65,7 @@ def test_numpy_oracle_input_gradients_match_reference(case):
     gin = {}
     on.loss_and_grads(params, z["in_x"], z["in_edge_index"], z["in_edge_attr"], batch,
                       z["in_y"], meta["depth"], meta["act"], meta["skip"],
-                      num_graphs=len(z["in_ptr"]) - 1, inputs_out=gin)
+                      num_graphs=len(z["in_ptr"]) - 1, inputs_out=gin, **_modes(meta))
     assert gin["x"].shape == z["gin_x"].shape
     assert gin["edge_attr"].shape == z["gin_edge_attr"].shape
     assert rel_err(gin["x"], z["gin_x"]) < 1e-5
@@ -69,6 +76,8 @@ def test_numpy_oracle_input_gradients_match_reference(case):
 @pytest.mark.parametrize("case", CASES)
 def test_torch_restatement_is_bitwise_reference(case):
     z, meta = load_golden(case)
+    if _modes(meta) != {"aggr": "add", "pool": "add"}:
+        pytest.skip("the torch restatement (CPU baseline) covers the reference defaults only")
     params, batch = _inputs(z, meta)
     m = TorchRestatement(params, meta["depth"], ACT[meta["act"]], meta["skip"])
     m.eval()
