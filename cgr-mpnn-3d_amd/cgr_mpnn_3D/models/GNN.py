@@ -32,9 +32,10 @@ import torch.nn.functional as F
 from .._amd import config as _config
 from .._amd import native
 from .._amd.functional import gnn_forward, gnn_predict
-from .._amd.pool import aggregation_code, global_add_pool, global_mean_pool, pooling_code
+from .._amd.pool import (aggregation_code, global_add_pool, global_max_pool, global_mean_pool,
+                         pooling_code)
 
-__all__ = ["GNN", "DMPNNConv", "global_add_pool", "global_mean_pool"]
+__all__ = ["GNN", "DMPNNConv", "global_add_pool", "global_mean_pool", "global_max_pool"]
 
 
 def _activation_code(fn) -> int:

@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
     const float* __restrict__ dy, const float* __restrict__ wf, const int* __restrict__ node_graph,
     const float* __restrict__ hn, const float* __restrict__ zn, int64_t N, int H, int Hp, int act,
     float* __restrict__ dzn, int colblocks, int cimg, b3_u4* __restrict__ img,
-    const float* __restrict__ gscale) {
+    const float* __restrict__ gscale, const int* __restrict__ pool_arg) {
   __shared__ float tile[32][kImgCols + 1];
   const int64_t s = blockIdx.x / colblocks;
   const int c0 = (int)(blockIdx.x - s * colblocks) * kImgCols;
@@ -285,6 +285,13 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
       o.y = d * wf[min(n + 1, H - 1)];
       o.z = d * wf[min(n + 2, H - 1)];
       o.w = d * wf[min(n + 3, H - 1)];
+      if (pool_arg) {  // global_max_pool: the gradient of a column goes to its arg-max node
+        const int4 am = *reinterpret_cast<const int4*>(pool_arg + (int64_t)gv * Hp + n);
+        o.x = am.x == v ? o.x : 0.f;
+        o.y = am.y == v ? o.y : 0.f;
+        o.z = am.z == v ? o.z : 0.f;
+        o.w = am.w == v ? o.w : 0.f;
+      }
       if (act == ACT_RELU) {
         const float4 h = *reinterpret_cast<const float4*>(hn + off);
         o.x = h.x > 0.f ? o.x : 0.f;
@@ -309,13 +316,14 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
 
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
-                           float* dzn, void* img, hipStream_t st, const float* gscale) {
+                           float* dzn, void* img, hipStream_t st, const float* gscale,
+                           const int* pool_arg) {
   if (N <= 0 || (!dzn && !img)) return hipSuccess;
   const int colblocks = (int)cdiv(Hp, kImgCols);
   const int64_t blocks = cdiv(N, 32) * colblocks;
   hipLaunchKernelGGL(k_readout_bwd_img, dim3((unsigned)blocks), dim3(256), 0, st, dy, wf,
                      node_graph, hn, zn, N, H, Hp, act, dzn, colblocks, b3_eimg_cols(H),
-                     static_cast<b3_u4*>(img), gscale);
+                     static_cast<b3_u4*>(img), gscale, pool_arg);
   return hipGetLastError();
 }
 

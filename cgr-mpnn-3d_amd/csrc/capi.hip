@@ -117,6 +117,7 @@ static void layout_prefix(const Dims& d, ArenaLayout& L, Bump& b) {
   L.xp = (d.F % 4 != 0) ? b.take(4 * N * (size_t)d.Fp) : kNone;
   L.inv_deg = d.aggr == CGR_AGGR_MEAN ? b.take(4 * N) : kNone;
   L.inv_cnt = d.pool == CGR_POOL_MEAN ? b.take(4 * B) : kNone;
+  L.pool_arg = d.pool == CGR_POOL_MAX ? b.take(4 * B * Hp) : kNone;
   // partial sums of the layer GEMMs' hub segments (over >= 3 row tiles), one slot pair per tile
   const size_t rt = (size_t)cdiv(d.E, b3nt_rows((int)d.E, d.H));
   L.fpart = b.take(4 * rt * 2 * 16 *
@@ -227,6 +228,7 @@ FloatView float_view(void* arena, const ArenaLayout& L, const Dims& d) {
   f.xp = (float*)at(arena, L.xp);
   f.inv_deg = (float*)at(arena, L.inv_deg);
   f.inv_cnt = (float*)at(arena, L.inv_cnt);
+  f.pool_arg = (int*)at(arena, L.pool_arg);
   for (int l = 0; l <= CGR_MAX_DEPTH; ++l) {
     f.h[l] = (float*)at(arena, L.h[l]);
     f.a[l] = (float*)at(arena, L.a[l]);
@@ -331,8 +333,9 @@ static int validate_config(const cgr_gnn_config* c) {
   CGR_CHECK(c->activation >= 0 && c->activation <= 2, "cgr: unknown activation code");
   CGR_CHECK(c->aggregation == CGR_AGGR_ADD || c->aggregation == CGR_AGGR_MEAN,
             "cgr: unknown aggregation (CGR_AGGR_ADD, CGR_AGGR_MEAN)");
-  CGR_CHECK(c->pooling == CGR_POOL_ADD || c->pooling == CGR_POOL_MEAN,
-            "cgr: unknown pooling (CGR_POOL_ADD, CGR_POOL_MEAN)");
+  CGR_CHECK(c->pooling == CGR_POOL_ADD || c->pooling == CGR_POOL_MEAN ||
+                c->pooling == CGR_POOL_MAX,
+            "cgr: unknown pooling (CGR_POOL_ADD, CGR_POOL_MEAN, CGR_POOL_MAX)");
   return 0;
 }
 

@@ -110,7 +110,7 @@ struct EpStoreRowScale {
   __device__ __forceinline__ Pre pre4(int r, int) const {
     const int rr = min(r, M - 1);
     const int g = node_graph[rr];
-    float s = dy[g];
+    float s = dy ? dy[g] : 1.f;  // (dy null: the A operand already holds it, max pooling)
     if (gscale) s *= gscale[g];
     if (nscale) s *= nscale[rr];
     return s;

@@ -198,20 +198,21 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // side: dwf, dbf; dzn; dW_n = dzn^T [x | s], db_n (forked before the main stream's readout NT:
   // deferring it behind a layer, or enqueuing the NT first, A/B -4..-14 %).  dzn is materialised
   // for the weight gradient only: the main stream's NT forms it inside the GEMM (LdActGrad).
+  // the split-bf16 e-image TN takes dzn as the e-image the dzn kernel writes (dzn itself is
+  // then never stored); the fp32 families read dzn
+  const bool ro_b3 =
+      fv.xp ? (b3tni_ok(LdConcat<4>{fv.xp, d.Fp, fv.a[D], Hp, d.Fp}, H, N) &&
+               ((uintptr_t)fv.xp & 15) == 0)
+            : (F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 &&
+               b3tni_ok(LdConcat<4>{b->x, F, fv.a[D], Hp, F}, H, N));
+  const bool max_pool = fv.pool_arg != nullptr;  // global_max_pool (CGR_POOL_MAX)
   auto side_readout = [&]() -> int {
     {  // dwf = dy^T g, dbf: off the main chain (step A/B +0.8 %)
       ProfScope _p("head_bwd", side);
       HIP_RET(head_bwd(dy, fv.g, params[CGR_PARAM_FFN_W(D)], d.B, H, Hp, nullptr,
                        grads[CGR_PARAM_FFN_W(D)], grads[CGR_PARAM_FFN_B(D)], side));
     }
-    // the split-bf16 e-image TN takes dzn as the e-image the dzn kernel writes (dzn itself is
-    // then never stored); the fp32 families read dzn
-    const bool ro_b3 =
-        fv.xp ? (b3tni_ok(LdConcat<4>{fv.xp, d.Fp, fv.a[D], Hp, d.Fp}, H, N) &&
-                 ((uintptr_t)fv.xp & 15) == 0)
-              : (F % 4 == 0 && ((uintptr_t)b->x & 15) == 0 &&
-                 b3tni_ok(LdConcat<4>{b->x, F, fv.a[D], Hp, F}, H, N));
-    {
+    if (!max_pool) {  // (max pooling: dzn and its image came from the main stream, below)
       ProfScope _p("readout_act_bwd", side);
       HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
                               Hp, d.act, ro_b3 ? nullptr : dzn, ro_b3 ? img_side : nullptr,
@@ -283,6 +284,12 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     ProfScope _p("gemm_nt_readout_bwd", st);
     const float* m = d.act == ACT_RELU ? fv.hn : fv.zn;
     const b3_u4* img = static_cast<const b3_u4*>(fv.b3rob);
+    if (max_pool) {  // ds = dzn W_n[:, F:] with dzn materialised (its per-element arg-max mask is
+                     // no row / column factor); the image is unscaled (gnn_fwd.hip)
+      const EpStoreRowScale ep{ds, Hp, N, H, nullptr, iv.node_graph, nullptr, fv.inv_deg};
+      HIP_RET(launch_b3nt(LdPlain<4>{dzn, Hp}, img, b3nt_cols(N, H), ep, N, H, H, st));
+      return 0;
+    }
     // (mean pooling: dy / graph count; mean aggregation: ds / in-degree, for dh_D = ds[dst])
     const EpStoreRowScale ep{ds, Hp, N, H, dy, iv.node_graph, fv.inv_cnt, fv.inv_deg};
     const B3Cols rc = b3nt_cols(N, H);  // the image's tiling (gnn_fwd.hip)
@@ -299,6 +306,11 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   // recorded before it, the side work after -- same dependencies) moves the NT onto the forward's
   // hardware queue in a captured graph but puts the first layer NT beside the readout TN: r05
   // same-box A/B 344.0k -> 341.0k reactions/s (3 runs each, profiles/r05_ro_first_ab.txt)
+  if (max_pool) {  // dzn (fp32 for the NT, and the TN's e-image) before the fork
+    ProfScope _p("readout_act_bwd", st);
+    HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H, Hp,
+                            d.act, dzn, ro_b3 ? img_side : nullptr, st, nullptr, fv.pool_arg));
+  }
   if (side != st) HIP_RET(fork_to(ss, st, side));
   if (const int rc = side_readout()) return rc;
   if (const int rc = readout_nt()) return rc;
@@ -574,7 +586,7 @@ int gnn_input_grads_impl(const Dims& d, const float* const* params, const void* 
       ProfScope _p("input_grad_prep", st);
       HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, H, Gs, Hp, st));
       HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
-                              Hp, d.act, dzn, nullptr, st, fv.inv_cnt));
+                              Hp, d.act, dzn, nullptr, st, fv.inv_cnt, fv.pool_arg));
       TransposeJobs tj{};  // wxT [F, ldw] = [W0[:, :F]^T | W_n[:, :F]^T]
       tj.job[0] = TransposeJob{params[CGR_PARAM_EDGE_INIT_W], F + Fe, 0, wxT, ldw, H, F};
       tj.job[1] = TransposeJob{params[CGR_PARAM_E2N_W(D)], F + H, 0, wxT + H, ldw, H, F};

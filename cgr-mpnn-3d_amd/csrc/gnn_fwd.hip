@@ -174,7 +174,8 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
                           st));
     if (!mode.eval && (training & CGR_TRAIN_FOR_BACKWARD)) {  // the backward NT GEMMs' W^T images
       B3PackJob rob = b3_job(Wn + F, 1, F + H, H, H, fv.b3rob, rcols);  // scaled by wf: LdActGrad
-      rob.kscale = params[CGR_PARAM_FFN_W(D)];
+      // (max pooling: the readout backward NT reads the materialised dzn, wf already in it)
+      if (d.pool != CGR_POOL_MAX) rob.kscale = params[CGR_PARAM_FFN_W(D)];
       HIP_RET(b3_pack_add(pm, rob, st));
       for (int l = 0; l < D; ++l)
         HIP_RET(b3_pack_add(pm, b3_job(params[CGR_PARAM_CONV_W(l)], 1, H, H, H, fv.b3lb[l], lcols),
@@ -339,7 +340,7 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
   ProfScope _p("pool_head_fwd", st);
   HIP_RET(pool_head_fwd(fv.hn, Hp, iv.graph_ptr, d.B, H, params[CGR_PARAM_FFN_W(D)],
-                        params[CGR_PARAM_FFN_B(D)], fv.g, y, st, fv.inv_cnt));
+                        params[CGR_PARAM_FFN_B(D)], fv.g, y, st, fv.inv_cnt, fv.pool_arg));
   return 0;
 }
 

@@ -82,6 +82,7 @@ struct FloatView {
   float* g;                       // [B, Hp] pooled graph embeddings
   float* inv_deg;  // [N] 1 / max(in-degree, 1)   (mean aggregation; else nullptr)
   float* inv_cnt;  // [B] 1 / max(graph nodes, 1) (mean pooling; else nullptr)
+  int* pool_arg;   // [B, Hp] max pooling's first arg-max node per column (else nullptr)
   // split-bf16 weight images (gemm_b3.hpp), packed once per step by the forward:
   void* b3x;                      // [W0[:, :F]; W_n[:, :F]]   (x-GEMM)
   void* b3rof;                    // W_n[:, F:]                 (readout forward)
@@ -109,6 +110,7 @@ struct ArenaLayout {
   size_t e_s, w0eT, P, Q, xp, h[CGR_MAX_DEPTH + 1], a[CGR_MAX_DEPTH + 1],
       pre[CGR_MAX_DEPTH + 1], zn, hn, g;
   size_t inv_deg, inv_cnt;  // mean aggregation / pooling: 1 / max(count, 1) per node / graph
+  size_t pool_arg;          // max pooling: [B, Hp] node of each pooled value (-1: empty graph)
   size_t b3x, b3rof, b3rob, b3lf[CGR_MAX_DEPTH], b3lb[CGR_MAX_DEPTH];
 };
 

@@ -342,7 +342,8 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
                                                             const float* __restrict__ bf,
                                                             float* __restrict__ g,
                                                             float* __restrict__ y,
-                                                            const float* __restrict__ inv_cnt) {
+                                                            const float* __restrict__ inv_cnt,
+                                                            int* __restrict__ pool_arg) {
   const int b = blockIdx.x;
   const int v0 = gptr[b], v1 = gptr[b + 1];
   const int C4 = Hp >> 2;
@@ -351,15 +352,34 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
   for (int c = threadIdx.x; c < C4; c += kPoolThreads) {
     const float* col = hn + 4 * c;
     float4 s = f4zero();
-    for (int v = v0; v < v1; v += kPoolBatch) {
-      float4 x[kPoolBatch];
+    if (pool_arg) {  // global_max_pool: the largest value, its first node (empty graph: 0, -1)
+      float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      int arg[4] = {-1, -1, -1, -1};
+      for (int v = v0; v < v1; ++v) {
+        const float4 x = *reinterpret_cast<const float4*>(col + (int64_t)v * Hp);
+        const float xv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-      for (int u = 0; u < kPoolBatch; ++u)
-        x[u] = v + u < v1 ? *reinterpret_cast<const float4*>(col + (int64_t)(v + u) * Hp)
-                          : f4zero();
+        for (int k = 0; k < 4; ++k)
+          if (xv[k] > m[k] || arg[k] < 0) {
+            m[k] = xv[k];
+            arg[k] = v;
+          }
+      }
+      if (v1 <= v0) m[0] = m[1] = m[2] = m[3] = 0.f;
+      s = make_float4(m[0], m[1], m[2], m[3]);
+      *reinterpret_cast<int4*>(pool_arg + (int64_t)b * Hp + 4 * c) =
+          make_int4(arg[0], arg[1], arg[2], arg[3]);
+    } else {
+      for (int v = v0; v < v1; v += kPoolBatch) {
+        float4 x[kPoolBatch];
 #pragma unroll
-      for (int u = 0; u < kPoolBatch; ++u)
-        if (v + u < v1) s = f4add(s, x[u]);
+        for (int u = 0; u < kPoolBatch; ++u)
+          x[u] = v + u < v1 ? *reinterpret_cast<const float4*>(col + (int64_t)(v + u) * Hp)
+                            : f4zero();
+#pragma unroll
+        for (int u = 0; u < kPoolBatch; ++u)
+          if (v + u < v1) s = f4add(s, x[u]);
+      }
     }
     if (inv_cnt) s = make_float4(s.x * gs, s.y * gs, s.z * gs, s.w * gs);
     *reinterpret_cast<float4*>(g + (int64_t)b * Hp + 4 * c) = s;
@@ -383,10 +403,10 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
 
 hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
                          const float* wf, const float* bf, float* g, float* y, hipStream_t st,
-                         const float* inv_cnt) {
+                         const float* inv_cnt, int* pool_arg) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pool_head, dim3(B), dim3(kPoolThreads), 0, st, hn, Hp, gptr, H, wf, bf, g,
-                     y, inv_cnt);
+                     y, inv_cnt, pool_arg);
   return hipGetLastError();
 }
 

@@ -45,10 +45,11 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
                          const float* w0eT, const float* b0, int64_t E, int H, int Hp, int act,
                          float* h0, float* pre0, hipStream_t st);
 
-// g[b] = sum_{v in graph b} hn[v] (* inv_cnt[b]: mean pooling, nullable);  y[b] = g[b] . wf + bf
+// g[b] = sum_{v in graph b} hn[v] (* inv_cnt[b]: mean pooling, nullable; pool_arg non-null:
+// max pooling, per column the max and its first node into pool_arg [B, Hp]);  y[b] = g[b].wf + bf
 hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
                          const float* wf, const float* bf, float* g, float* y, hipStream_t st,
-                         const float* inv_cnt = nullptr);
+                         const float* inv_cnt = nullptr, int* pool_arg = nullptr);
 
 // mean aggregation / pooling factors: inv_deg[v] = 1 / max(in-degree, 1) from the dst CSR,
 // inv_cnt[b] = 1 / max(nodes of graph b, 1) (either nullable: not computed)
@@ -63,10 +64,12 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
 
 // dzn[v] = dy[graph(v)] * wf * act'(zn[v])   (ReLU: hn > 0)
 // dzn (may be null: not materialised) and/or its e-image `img` (gemm_b3.hpp B3EImg; null: none)
-// gscale (nullable): per-graph factor of dy (mean pooling: inv_cnt)
+// gscale (nullable): per-graph factor of dy (mean pooling: inv_cnt); pool_arg (nullable): max
+// pooling, dzn[v, n] kept only where v is the graph's arg-max node of column n
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
-                           float* dzn, void* img, hipStream_t st, const float* gscale = nullptr);
+                           float* dzn, void* img, hipStream_t st, const float* gscale = nullptr,
+                           const int* pool_arg = nullptr);
 
 struct LayerBwdArgs {
   // dh_{l+1}: top layer (l == D-1, layer_act_bwd): ds[dst_s[i]]; below (the fused dm GEMM,

@@ -59,9 +59,10 @@ typedef struct cgr_gnn_config {
 /* aggr of GNN.__init__ / DMPNNConv (PyG MessagePassing): "add" (= "sum", the default) or "mean"
  * (the sum over a node's in-edges divided by their count, 0 for a node without in-edges) */
 enum cgr_aggregation { CGR_AGGR_ADD = 0, CGR_AGGR_MEAN = 1 };
-/* pooling_fn: global_add_pool (default) or global_mean_pool (the graph's node sum divided by its
- * node count) */
-enum cgr_pooling { CGR_POOL_ADD = 0, CGR_POOL_MEAN = 1 };
+/* pooling_fn: global_add_pool (default), global_mean_pool (the graph's node sum divided by its
+ * node count) or global_max_pool (per column the largest node value; its gradient goes to the
+ * first node holding it) */
+enum cgr_pooling { CGR_POOL_ADD = 0, CGR_POOL_MEAN = 1, CGR_POOL_MAX = 2 };
 
 /* One collated batch, the fields GNN.forward reads from a PyG Batch (GNN.py:77-82). */
 typedef struct cgr_batch {

@@ -120,9 +120,11 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     """GNN.forward (GNN.py:76-110) in float64. Returns (y[B], cache).
 
     ``aggr`` ("add" / "mean"): DMPNNConv's PyG aggregation (GNN.py:22,63,119); ``pool`` ("add" /
-    "mean"): global_add_pool / global_mean_pool (GNN.py:23,110).  PyG's mean is the sum divided
-    by max(count, 1) (torch_geometric.utils.scatter, reduce="mean"; PyG is absent here, its
-    semantics restated).
+    "mean" / "max"): global_add_pool / global_mean_pool / global_max_pool (GNN.py:23,110).  PyG's
+    mean is the sum divided by max(count, 1) (torch_geometric.utils.scatter, reduce="mean"), its
+    max a column-wise amax whose gradient this restatement gives to the first arg-max node
+    (PyG is absent here, its semantics restated; ties do not occur on continuous data except at
+    ReLU's exact zeros, whose gradient the activation zeroes anyway).
 
     ``params`` uses the reference ``state_dict`` keys.  ``dropout_masks[l]`` (optional, 0/1 per
     element of h) + ``dropout_ps[l]`` reproduce ``F.dropout`` in train mode with a given mask.
@@ -143,7 +145,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     sig = [float(np.asarray(params[f"skip_weights.{l}"])) if learnable_skip else 1.0
            for l in range(depth)]
     rev = np.arange(E) ^ 1
-    assert aggr in ("add", "sum", "mean") and pool in ("add", "mean")
+    assert aggr in ("add", "sum", "mean") and pool in ("add", "mean", "max")
     inv_deg = np.ones(N)
     if aggr == "mean":
         inv_deg = 1.0 / np.maximum(np.bincount(dst, minlength=N)[:N], 1)
@@ -191,9 +193,19 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
         B = int(num_graphs if num_graphs is not None else gid.max() + 1)
         g = _scatter_sum(hnode, gid, B)  # GNN.py:110 global_add_pool
     inv_cnt = np.ones(B)
+    pool_arg = None
     if pool == "mean":  # global_mean_pool
         inv_cnt = 1.0 / np.maximum(np.bincount(gid, minlength=B)[:B], 1)
         g = g * inv_cnt[:, None]
+    elif pool == "max":  # global_max_pool: column max per graph, the gradient to its first node
+        g = np.zeros((B, hnode.shape[1]))
+        pool_arg = np.full((B, hnode.shape[1]), -1, dtype=np.int64)
+        for b in range(B):
+            nodes = np.nonzero(gid == b)[0]
+            if nodes.size:
+                k = np.argmax(hnode[nodes], axis=0)  # first occurrence of the max
+                pool_arg[b] = nodes[k]
+                g[b] = hnode[nodes[k], np.arange(hnode.shape[1])]
     wf = np.asarray(params["ffn.weight"], f8)  # [1, H]
     bf = np.asarray(params["ffn.bias"], f8)
     y = (g @ wf.T + bf)[:, 0]
@@ -201,7 +213,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
                  zs=zs, s=s, qn=qn, zn=zn, hnode=hnode, g=g, gid=gid, B=B, sig=sig, N=N, E=E,
                  depth=depth, act=act, learnable_skip=learnable_skip,
                  masks=dropout_masks, ps=dropout_ps, relu_masks=rm, inv_deg=inv_deg,
-                 inv_cnt=inv_cnt)
+                 inv_cnt=inv_cnt, pool_arg=pool_arg)
     return y, cache
 
 
@@ -230,6 +242,8 @@ def backward(params: dict, cache: dict, dy: np.ndarray, inputs_out: dict | None 
 
     inv_deg, inv_cnt = cache["inv_deg"], cache["inv_cnt"]
     dhnode = (dg * inv_cnt[:, None])[cache["gid"]]  # pooling backward = gather by graph id
+    if cache.get("pool_arg") is not None:  # max pooling: only each column's arg-max node
+        dhnode = dhnode * (cache["pool_arg"][cache["gid"]] == np.arange(N)[:, None])
     dzn = dhnode * grad_of(cache["zn"], "zn")
     grads["edge_to_node.weight"] = dzn.T @ cache["qn"]
     grads["edge_to_node.bias"] = dzn.sum(0)

@@ -82,12 +82,24 @@ def _global_mean_pool(x, batch, size=None):
     return _scatter_mean(x, batch, size)
 
 
+def _global_max_pool(x, batch, size=None):
+    # PyG utils.scatter(reduce="max") without torch_scatter: scatter_reduce amax, include_self=False
+    if batch is None:
+        return x.max(dim=-2, keepdim=x.dim() == 2)[0]
+    if size is None:
+        size = int(batch.max()) + 1 if batch.numel() > 0 else 0
+    idx = batch.view(-1, *([1] * (x.dim() - 1))).expand_as(x)
+    return x.new_zeros((size,) + tuple(x.shape[1:])).scatter_reduce(0, idx, x, reduce="amax",
+                                                                    include_self=False)
+
+
 def _install_pyg_standin():
     tg = types.ModuleType("torch_geometric")
     tgnn = types.ModuleType("torch_geometric.nn")
     tgnn.MessagePassing = _MessagePassing
     tgnn.global_add_pool = _global_add_pool
     tgnn.global_mean_pool = _global_mean_pool
+    tgnn.global_max_pool = _global_max_pool
     tg.nn = tgnn
     sys.modules["torch_geometric"] = tg
     sys.modules["torch_geometric.nn"] = tgnn
@@ -147,6 +159,10 @@ CASES = {
     "mean_both_gelu_none": (dict(num_graphs=1, n_atoms=16, n_bonds=17, n_mace=0, seed=22),
                             dict(depth=2, hidden=24, act="gelu", skip=False),
                             {"aggr": "mean", "pool": "mean", "batch_none": True}),
+    # pooling_fn=global_max_pool, smooth activation (no ties), ragged graphs
+    "max_pool_silu": (dict(num_graphs=5, n_atoms=16, n_bonds=18, n_mace=8, seed=23,
+                           n_atoms_jitter=6),
+                      dict(depth=3, hidden=32, act="silu", skip=False), {"pool": "max"}),
 }
 
 
@@ -168,6 +184,8 @@ def run_case(ref, name, bkw, mkw, extra):
         kw["aggr"] = extra["aggr"]
     if extra.get("pool") == "mean":
         kw["pooling_fn"] = _global_mean_pool
+    if extra.get("pool") == "max":
+        kw["pooling_fn"] = _global_max_pool
     model = ref.GNN(x.shape[1], ea.shape[1], depth=D, hidden_sizes=[H] * D,
                     dropout_ps=[p_eval] * D, activation_fn=ACTS[mkw["act"]],
                     use_learnable_skip=mkw["skip"], **kw)

@@ -62,9 +62,9 @@ SKIP_COND_U = 2.0 ** -20
 
 
 def _pool_fn(pool):
-    from cgr_mpnn_3D.models.GNN import global_add_pool, global_mean_pool
+    from cgr_mpnn_3D.models.GNN import global_add_pool, global_max_pool, global_mean_pool
 
-    return global_mean_pool if pool == "mean" else global_add_pool
+    return {"add": global_add_pool, "mean": global_mean_pool, "max": global_max_pool}[pool]
 
 
 def model_from_golden(z, meta, dev, dropout=None):
@@ -181,7 +181,7 @@ def test_edge_feature_widths_vs_oracle(Fe, cuda_device):
 
 def _cfg_tuple(F_, Fe, H, D, act, skip, aggr="add", pool="add"):
     return (F_, Fe, H, D, {"relu": 0, "silu": 1, "gelu": 2}[act], skip,
-            {"add": 0, "mean": 1}[aggr], {"add": 0, "mean": 1}[pool])
+            {"add": 0, "mean": 1}[aggr], {"add": 0, "mean": 1, "max": 2}[pool])
 
 
 def _graph_prep_check(b, dev, use_ptr=True, batch_none=False):
@@ -1009,7 +1009,9 @@ def test_unpaired_batch_after_paired_ones_warns_without_a_sync(cuda_device):
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("aggr,pool,act,skip", [("mean", "add", "relu", False),
                                                 ("add", "mean", "silu", True),
-                                                ("mean", "mean", "gelu", False)])
+                                                ("mean", "mean", "gelu", False),
+                                                ("add", "max", "relu", False),
+                                                ("mean", "max", "silu", True)])
 def test_mean_modes_cfg2_widths_vs_oracle(aggr, pool, act, skip, cuda_device):
     _oracle_compare(make_batch(32, seed=24, n_atoms_jitter=8), 400, 4, act, skip, cuda_device,
                     inputs=True, aggr=aggr, pool=pool)
@@ -1043,6 +1045,27 @@ def test_mean_modes_isolated_nodes_and_predict_path(cuda_device):
     with torch.no_grad():
         y_eval = m(data)
     assert torch.equal(y_train, y_eval)
+
+
+def test_max_pooling_standalone_function_matches_native_head(cuda_device):
+    # the module's global_max_pool (PyG semantics, torch ops) applied to the native model's node
+    # rows equals the native fused head's pooled value: y = ffn(max-pool(h))
+    from cgr_mpnn_3D.models.GNN import global_max_pool
+
+    b = make_batch(6, n_mace=8, seed=36, n_atoms_jitter=5)
+    torch.manual_seed(2)
+    m = GNN(b.x.shape[1], 14, depth=2, hidden_sizes=[32, 32], dropout_ps=[0.0, 0.0],
+            activation_fn=F.silu, pooling_fn=global_max_pool).to(cuda_device).train()
+    data = b.to_torch(cuda_device)
+    F_ = b.x.shape[1]
+    run = ArenaRun(_cfg_tuple(F_, 14, 32, 2, "silu", False, "add", "max"), data.x,
+                   data.edge_index, data.edge_attr, data.batch, data.ptr, b.num_graphs,
+                   [p.detach() for p in m.native_parameters()])
+    torch.cuda.synchronize()
+    hn = run.floats("hn", b.x.shape[0])[:, :32]
+    g = global_max_pool(hn, data.batch)
+    y_ref = g @ m.ffn.weight.detach().t() + m.ffn.bias.detach()
+    assert torch.allclose(run.y, y_ref[:, 0], rtol=1e-6, atol=1e-6)
 
 
 def test_unsupported_aggregation_and_pooling_raise(cuda_device):
