@@ -14,7 +14,7 @@ from . import native
 
 class _DMPNNConvFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, edge_index, h, weight, bias, num_nodes):
+    def forward(ctx, edge_index, h, weight, bias, num_nodes, aggregation):
         lib = native.load()
         E, H = int(h.shape[0]), int(h.shape[1])
         dev = h.device
@@ -26,9 +26,10 @@ class _DMPNNConvFunction(torch.autograd.Function):
             native.check(lib.cgr_dmpnn_conv_forward(
                 native.ptr(edge_index), num_nodes, E, native.ptr(h), H, native.ptr(weight),
                 native.ptr(bias), native.ptr(a), native.ptr(out), native.ptr(scratch),
-                native.stream_ptr(dev)))
+                int(aggregation), native.stream_ptr(dev)))
         ctx.save_for_backward(edge_index, h, weight, scratch)
         ctx.num_nodes = num_nodes
+        ctx.aggregation = int(aggregation)
         return a, out
 
     @staticmethod
@@ -46,11 +47,12 @@ class _DMPNNConvFunction(torch.autograd.Function):
             native.check(lib.cgr_dmpnn_conv_backward(
                 native.ptr(edge_index), ctx.num_nodes, E, native.ptr(h), H, native.ptr(weight),
                 native.ptr(ga), native.ptr(go), native.ptr(gh), native.ptr(gw), native.ptr(gb),
-                native.ptr(scratch), native.stream_ptr(dev)))
-        return None, gh, gw, gb, None
+                native.ptr(scratch), ctx.aggregation, native.stream_ptr(dev)))
+        return None, gh, gw, gb, None, None
 
 
-def dmpnn_conv(edge_index, h, weight, bias):
+def dmpnn_conv(edge_index, h, weight, bias, aggregation=0):
+    """aggregation: 0 "add" (= "sum"), 1 "mean" (include/cgr_mpnn3d.h enum cgr_aggregation)."""
     if not h.is_cuda:
         raise RuntimeError("cgr_mpnn_3D (MI355X): DMPNNConv runs on the GPU only (no CPU fallback)")
     edge_index = edge_index.to(device=h.device, dtype=torch.int64).contiguous()
@@ -59,4 +61,4 @@ def dmpnn_conv(edge_index, h, weight, bias):
     num_nodes = int(edge_index[1].max()) + 1  # PyG's inferred dim_size (x=None at GNN.py:134)
     return _DMPNNConvFunction.apply(edge_index, h.float().contiguous(),
                                     weight.float().contiguous(), bias.float().contiguous(),
-                                    num_nodes)
+                                    num_nodes, aggregation)

@@ -94,10 +94,10 @@ SIGNATURES = [
     ("cgr_dmpnn_conv_scratch_bytes", c_int64, [c_int64, c_int64, c_int64]),
     ("cgr_dmpnn_conv_forward", c_int32,
      [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-      c_void_p, c_void_p]),
+      c_void_p, c_int32, c_void_p]),
     ("cgr_dmpnn_conv_backward", c_int32,
      [c_void_p, c_int64, c_int64, c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
-      c_void_p, c_void_p, c_void_p, c_void_p]),
+      c_void_p, c_void_p, c_void_p, c_int32, c_void_p]),
     ("cgr_adam_step", c_int32,
      [POINTER(CgrAdamTensor), c_int32, c_double, c_double, c_double, c_double, c_double, c_int32,
       c_int32, c_void_p]),

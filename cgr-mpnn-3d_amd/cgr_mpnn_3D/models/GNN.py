@@ -274,9 +274,8 @@ class DMPNNConv(nn.Module):
     def forward(self, edge_index, edge_attr):
         from .._amd.conv import dmpnn_conv
 
-        if self.aggr != "add":
-            raise NotImplementedError("DMPNNConv (MI355X): only aggr='add' is native")
-        return dmpnn_conv(edge_index, edge_attr, self.lin.weight, self.lin.bias)
+        return dmpnn_conv(edge_index, edge_attr, self.lin.weight, self.lin.bias,
+                          aggregation_code(self.aggr))
 
     def message(self, edge_attr):
         return edge_attr

@@ -1,5 +1,6 @@
 // Standalone DMPNNConv (GNN.py:113-145) on the native kernels, in the caller's edge order:
-//   a[v]  = sum_{dst(e) = v} h[e]                    (propagate, aggr="add", dim_size = N)
+//   a[v]  = sum_{dst(e) = v} h[e]                    (propagate, aggr="add", dim_size = N;
+//                                                     aggr="mean": / max(in-degree, 1))
 //   h'[e] = (a[src(e)] - h[e ^ 1]) W^T + b           (GNN.py:136-141)
 // and its reverse mode.  GNN.forward never calls this (the fused path inlines the layer); it keeps
 // the reference's public DMPNNConv usable on its own.
@@ -18,7 +19,7 @@ namespace {
 
 struct ConvLayout {
   size_t src_c, dst_c, perm, dst_ptr, src_perm, src_ptr, deg, cursor;  // ints
-  size_t h_p, a_p, dout_p, dm, da, wT, slab, bslab;                    // floats
+  size_t h_p, a_p, dout_p, dm, da, wT, slab, bslab, inv_deg;           // floats
   size_t bytes;
 };
 
@@ -48,6 +49,7 @@ ConvLayout conv_layout(int64_t N, int64_t E, int64_t H) {
   const TnPlan p = tn_plan((int)H, (int)H, (int)E);
   L.slab = take(4 * (size_t)p.splits * H * (size_t)((H + 3) & ~3));  // slab rows padded to 4
   L.bslab = take(4 * (size_t)p.splits * H);
+  L.inv_deg = take(4 * N);
   L.bytes = off;
   return L;
 }
@@ -67,15 +69,17 @@ __global__ void k_add_rows(float* __restrict__ da, int64_t N, int H, int Hp,
   da[v * Hp + c] += g[t];
 }
 
-// dh[e, :H] = da[dst(e)] - dm[e ^ 1]
+// dh[e, :H] = da[dst(e)] (* inv_deg[dst(e)]: mean) - dm[e ^ 1]
 __global__ void k_conv_dh(const float* __restrict__ da, const float* __restrict__ dm,
                           const int* __restrict__ dst_c, int64_t E, int H, int Hp,
-                          float* __restrict__ dh) {
+                          float* __restrict__ dh, const float* __restrict__ inv_deg) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= E * H) return;
   const int64_t e = t / H;
   const int c = (int)(t - e * H);
-  dh[t] = da[(int64_t)dst_c[e] * Hp + c] - dm[(e ^ 1) * Hp + c];
+  const int v = dst_c[e];
+  const float s = inv_deg ? inv_deg[v] : 1.f;
+  dh[t] = da[(int64_t)v * Hp + c] * s - dm[(e ^ 1) * Hp + c];
 }
 
 }  // namespace
@@ -92,10 +96,12 @@ int64_t cgr_dmpnn_conv_scratch_bytes(int64_t num_nodes, int64_t num_edges, int64
 
 int cgr_dmpnn_conv_forward(const int64_t* edge_index, int64_t N, int64_t E, const float* h,
                            int64_t H, const float* weight, const float* bias, float* a_out,
-                           float* h_out, void* scratch, void* stream) {
+                           float* h_out, void* scratch, int32_t aggregation, void* stream) {
   clear_stale_hip_error();
   CGR_CHECK(edge_index && h && weight && bias && a_out && h_out && scratch,
             "cgr_dmpnn_conv_forward: NULL pointer");
+  CGR_CHECK(aggregation == CGR_AGGR_ADD || aggregation == CGR_AGGR_MEAN,
+            "cgr_dmpnn_conv_forward: unknown aggregation");
   CGR_CHECK(N >= 1 && E >= 2 && E % 2 == 0 && H >= 1 && E < (1ll << 30) && N < (1ll << 31),
             "cgr_dmpnn_conv_forward: bad sizes (E must be even and > 0)");
   hipStream_t st = (hipStream_t)stream;
@@ -116,6 +122,11 @@ int cgr_dmpnn_conv_forward(const int64_t* edge_index, int64_t N, int64_t E, cons
   HIP_RET(hipMemcpy2DAsync(h_p, Hp * 4, h, H * 4, H * 4, E, hipMemcpyDeviceToDevice, st));
   HIP_RET(segment_sum(h_p, Hp, P<int>(scratch, L.perm), P<int>(scratch, L.dst_ptr), N, Hp, a_p,
                       Hp, st));
+  if (aggregation == CGR_AGGR_MEAN) {  // the mean: a / max(in-degree, 1), kept for the backward
+    float* inv = P<float>(scratch, L.inv_deg);
+    HIP_RET(mean_scales(P<int>(scratch, L.dst_ptr), N, nullptr, 0, inv, nullptr, st));
+    HIP_RET(scale_rows(a_p, Hp, N, inv, st));
+  }
   HIP_RET(hipMemcpy2DAsync(a_out, H * 4, a_p, Hp * 4, H * 4, N, hipMemcpyDeviceToDevice, st));
   const int vw = vec_for(weight, H, H);
   hipError_t e = with_vec(vw, [&](auto VW) {
@@ -133,12 +144,14 @@ int cgr_dmpnn_conv_forward(const int64_t* edge_index, int64_t N, int64_t E, cons
 int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t N, int64_t E, const float* h,
                             int64_t H, const float* weight, const float* grad_a,
                             const float* grad_h_out, float* grad_h, float* grad_weight,
-                            float* grad_bias, void* scratch, void* stream) {
+                            float* grad_bias, void* scratch, int32_t aggregation, void* stream) {
   clear_stale_hip_error();
   (void)edge_index;
   (void)h;
   CGR_CHECK(weight && grad_h && grad_weight && grad_bias && scratch,
             "cgr_dmpnn_conv_backward: NULL pointer");
+  CGR_CHECK(aggregation == CGR_AGGR_ADD || aggregation == CGR_AGGR_MEAN,
+            "cgr_dmpnn_conv_backward: unknown aggregation");
   CGR_CHECK(N >= 1 && E >= 2 && E % 2 == 0 && H >= 1, "cgr_dmpnn_conv_backward: bad sizes");
   hipStream_t st = (hipStream_t)stream;
   const ConvLayout L = conv_layout(N, E, H);
@@ -193,7 +206,8 @@ int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t N, int64_t E, con
     HIP_RET(hipGetLastError());
   }
   hipLaunchKernelGGL(k_conv_dh, dim3(cdiv(E * H, 256)), dim3(256), 0, st, da, dm, dst_c, E, (int)H,
-                     Hp, grad_h);
+                     Hp, grad_h,
+                     aggregation == CGR_AGGR_MEAN ? P<float>(scratch, L.inv_deg) : nullptr);
   HIP_RET(hipGetLastError());
   return 0;
 }

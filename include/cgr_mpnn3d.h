@@ -213,19 +213,22 @@ int cgr_segment_sum(const float* values, int64_t ld_values, const int32_t* index
                     int64_t ld_out, void* stream);
 
 /* DMPNNConv.forward(edge_index, edge_attr) -> (a, h') (GNN.py:131-141), in the caller's edge
- * order: a[v] = sum_{dst(e)=v} h[e] (dim_size = N), h'[e] = (a[src(e)] - h[e^1]) W^T + b.
+ * order: a[v] = sum_{dst(e)=v} h[e] (dim_size = N; aggregation CGR_AGGR_MEAN: divided by
+ * max(in-degree, 1)), h'[e] = (a[src(e)] - h[e^1]) W^T + b.
  * `scratch` needs cgr_dmpnn_conv_scratch_bytes(N, E, H). */
 int64_t cgr_dmpnn_conv_scratch_bytes(int64_t num_nodes, int64_t num_edges, int64_t hidden);
 int cgr_dmpnn_conv_forward(const int64_t* edge_index, int64_t num_nodes, int64_t num_edges,
                            const float* h, int64_t hidden, const float* weight, const float* bias,
-                           float* a_out, float* h_out, void* scratch, void* stream);
+                           float* a_out, float* h_out, void* scratch, int32_t aggregation,
+                           void* stream);
 /* Reverse mode of cgr_dmpnn_conv_forward given dL/da (may be NULL) and dL/dh' (may be NULL):
  * writes dL/dh [E,H], dL/dW [H,H], dL/db [H].  `scratch` must hold the forward's bookkeeping
  * (same scratch buffer, untouched since the forward) plus cgr_dmpnn_conv_scratch_bytes. */
 int cgr_dmpnn_conv_backward(const int64_t* edge_index, int64_t num_nodes, int64_t num_edges,
                             const float* h, int64_t hidden, const float* weight,
                             const float* grad_a, const float* grad_h_out, float* grad_h,
-                            float* grad_weight, float* grad_bias, void* scratch, void* stream);
+                            float* grad_weight, float* grad_bias, void* scratch,
+                            int32_t aggregation, void* stream);
 
 /* torch.optim.Adam(params, lr, betas, eps, weight_decay, amsgrad) step (train.py:117-119), fused
  * over every parameter tensor in one launch (+ one tiny launch for the step counter) instead of

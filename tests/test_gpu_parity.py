@@ -647,14 +647,14 @@ def test_segment_sum_api(width, ld, gather, cuda_device):
     assert not out.cpu().numpy()[:, width:].any()  # never writes past `width`
 
 
-@pytest.mark.parametrize("H", [32, 45])
-def test_dmpnn_conv_standalone_vs_torch_cpu(H, cuda_device):
+@pytest.mark.parametrize("H,aggr", [(32, "add"), (45, "add"), (40, "mean")])
+def test_dmpnn_conv_standalone_vs_torch_cpu(H, aggr, cuda_device):
     from cgr_mpnn_3D.models.GNN import DMPNNConv
 
     b = make_batch(5, n_atoms=11, n_bonds=13, n_mace=0, seed=H)
     E, N = b.edge_index.shape[1], b.x.shape[0]
     torch.manual_seed(H)
-    conv = DMPNNConv(H)
+    conv = DMPNNConv(H, aggr=aggr)
     h = torch.randn(E, H)
     ga = torch.randn(N, H)
     gh = torch.randn(E, H)
@@ -664,6 +664,8 @@ def test_dmpnn_conv_standalone_vs_torch_cpu(H, cuda_device):
     br = conv.lin.bias.detach().clone().requires_grad_(True)
     ei = torch.from_numpy(b.edge_index)
     a_ref = torch.zeros(N, H).index_add(0, ei[1], hr)
+    if aggr == "mean":  # PyG scatter mean: / max(count, 1)
+        a_ref = a_ref / torch.bincount(ei[1], minlength=N).clamp(min=1).float()[:, None]
     rev = torch.flip(hr.view(E // 2, 2, H), dims=[1]).reshape(E, H)
     out_ref = F.linear(a_ref[ei[0]] - rev, wr, br)
     (a_ref * ga).sum().backward(retain_graph=True)
