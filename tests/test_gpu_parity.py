@@ -703,13 +703,20 @@ def test_trainer_loop_reduces_loss(cuda_device):
     assert losses[-1] < 0.5 * losses[0]
 
 
-def test_cuda_graph_capture_replays_fwd_bwd(cuda_device):
+@pytest.mark.parametrize("aggr,pool,inputs", [("add", "add", False), ("mean", "max", True)])
+def test_cuda_graph_capture_replays_fwd_bwd(aggr, pool, inputs, cuda_device):
+    # (mean / max modes add their scaling launches and the arg-max pass, input gradients the
+    # cgr_gnn_input_grads launches: all inside the captured step)
     b = make_batch(32, seed=61)
     torch.manual_seed(0)
-    m = GNN(b.x.shape[1], 14, depth=4, hidden_sizes=[400] * 4, dropout_ps=[0.0] * 4)
+    m = GNN(b.x.shape[1], 14, depth=4, hidden_sizes=[400] * 4, dropout_ps=[0.0] * 4, aggr=aggr,
+            pooling_fn=_pool_fn(pool))
     m = m.to(cuda_device).train()
     data = b.to_torch(cuda_device)
     params = list(m.parameters())
+    if inputs:
+        data.x.requires_grad_(True)
+        params = params + [data.x]
 
     def step():
         pred = m(data)
@@ -1029,7 +1036,7 @@ def test_mean_aggregation_hub_segments_vs_oracle(cuda_device):
 def test_mean_aggregation_unpaired_vs_oracle(cuda_device):
     u = _shuffled_pairs(make_batch(8, n_atoms=30, n_bonds=30, n_mace=16, seed=33), seed=8)
     assert _pair_status(u, cuda_device) == 4
-    _oracle_compare(u, 64, 3, "relu", True, cuda_device, aggr="mean")
+    _oracle_compare(u, 64, 3, "relu", True, cuda_device, aggr="mean", inputs=True)
     torch.cuda.synchronize()
     native.raise_device_errors(cuda_device)
 
