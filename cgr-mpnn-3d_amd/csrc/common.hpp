@@ -17,6 +17,12 @@
 namespace cgr {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+// a float4 store marked non-temporal (global_store_dwordx4 ... nt): the forward layer GEMM's h and
+// a rows, streamed out by every workgroup's epilogue at once (same-box A/B +0.8 % on the step,
+// profiles/r05_nt_store_ab.txt; the backward's dpre rows stored this way ran 0.4 % slower)
+__device__ __forceinline__ void st4_nt(float* p, const float4& v) {
+  __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w}, reinterpret_cast<floatx4*>(p));
+}
 
 enum Act : int { ACT_RELU = 0, ACT_SILU = 1, ACT_GELU = 2 };
 

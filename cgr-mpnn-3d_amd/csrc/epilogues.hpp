@@ -201,7 +201,7 @@ struct EpLayer {
         h[k] *= scale;
     }
     const float4 hv = make_float4(h[0], h[1], h[2], h[3]);
-    *reinterpret_cast<float4*>(hout + o) = hv;
+    st4_nt(hout + o, hv);
     return hv;
   }
   // the addend (b + sigma h0) taken into the accumulators in the GEMM's MFMA layout

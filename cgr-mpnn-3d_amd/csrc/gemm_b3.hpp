@@ -724,7 +724,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
           sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * ec4, a);
         }
       } else {
-        *reinterpret_cast<float4*>(dst) = a;
+        st4_nt(dst, a);  // (common.hpp)
       }
     }
     // hub segments: the last contributor sums the slots of every row tile in order
