@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--config", default="cfg2",
                     choices=["cfg1", "cfg2", "cfg4", "cfg5", "train_default", "sweep_b16",
-                             "sweep_b64"])
+                             "sweep_b64", "sweep_d5", "sweep_max"])
     ap.add_argument("--graph", type=int, default=-1,
                     help="capture the step in a HIP graph (1/0; -1 = auto: on for N = 1)")
     ap.add_argument("--loss", default="fused", choices=["fused", "torch"],

@@ -196,4 +196,10 @@ CONFIGS = {
                       learnable_skip=False),
     "sweep_b64": dict(num_graphs=64, n_atoms=30, n_bonds=30, n_mace=768, depth=3, hidden=300,
                       learnable_skip=False),
+    # the sweep's depth 5 (sweep_config.json:6) at train.py's default width and batch, and the
+    # sweep's largest point: depth 6, hidden 1000, batch 64, learnable skip (:6-7, :12, :15)
+    "sweep_d5": dict(num_graphs=32, n_atoms=30, n_bonds=30, n_mace=768, depth=5, hidden=300,
+                     learnable_skip=False),
+    "sweep_max": dict(num_graphs=64, n_atoms=30, n_bonds=30, n_mace=768, depth=6, hidden=1000,
+                      learnable_skip=True),
 }
