@@ -233,7 +233,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         HIP_RET(b3tni_run("gemm_tn_wgrad_readout", img_side, bl, H, Fp + H, N, sl, bsl, true, &p,
                           side, kB3TnReadoutTarget, pend.job));
         RedJob j = mine;
-        j.splits = p.splits;
+        red_job_set_splits(j, p.splits);
         if (const int rc = fold(j, 0)) return rc;
       } else {
         if (tnr_x_ok(H, Fp + H, Fp, fv.xp)) {
@@ -245,7 +245,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
                           side));
         }
         RedJob j = mine;
-        j.splits = p.splits;
+        red_job_set_splits(j, p.splits);
         if (const int rc = unfolded(j, 0)) return rc;
       }
     } else {
@@ -255,7 +255,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         HIP_RET(b3tni_run("gemm_tn_wgrad_readout", img_side, bl4, H, F + H, N, sl, bsl, true, &p,
                           side, kB3TnReadoutTarget, pend.job));
         RedJob j = mine;
-        j.splits = p.splits;
+        red_job_set_splits(j, p.splits);
         if (const int rc = fold(j, 0)) return rc;
       } else {
         if (F % 4 == 0 && tnr_x_ok(H, F + H, F, b->x)) {
@@ -272,7 +272,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
           HIP_RET(e);
         }
         RedJob j = mine;
-        j.splits = p.splits;
+        red_job_set_splits(j, p.splits);
         if (const int rc = unfolded(j, 0)) return rc;
       }
     }
@@ -433,7 +433,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
       if (l == D - 1 && top_b3) {
         HIP_RET(b3tni_run("gemm_tn_wgrad_layer", img_top, bl, H, H, E, sl, bsl, true, &p, side,
                           kB3TnTarget, pend.job));
-        mine.splits = p.splits;
+        red_job_set_splits(mine, p.splits);
         if (const int rc = fold(mine, D - l)) return rc;
       } else if (b3tni_ok(bl, H, E)) {
         {
@@ -442,7 +442,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         }
         HIP_RET(b3tni_run("gemm_tn_wgrad_layer", img_side, bl, H, H, E, sl, bsl, true, &p, side,
                           kB3TnTarget, pend.job));
-        mine.splits = p.splits;
+        red_job_set_splits(mine, p.splits);
         if (const int rc = fold(mine, D - l)) return rc;
       } else {
         if (tf == 5) {
@@ -456,7 +456,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
         } else {
           HIP_RET(tn_gemm("gemm_tn_wgrad_layer", al, bl, H, H, E, sl, bsl, true, &p, side));
         }
-        mine.splits = p.splits;
+        red_job_set_splits(mine, p.splits);
         if (const int rc = unfolded(mine, D - l)) return rc;
       }
     }

@@ -544,6 +544,12 @@ __device__ __forceinline__ void reduce_slab_block(const RedJob& J, int blk, floa
   const int ldk = (J.Kout + 3) & ~3;
   const int c4n = ldk >> 2;
   const int64_t nf = (int64_t)J.Nout * c4n;
+  if (J.splits < kRedGroups) {
+    // fewer splits than groups: the grouped form would idle kRedGroups - splits groups, so each
+    // thread takes one float4 output (or bias element) and sums its splits in order
+    reduce_slab_item(J, (int64_t)blk * (kRedCols * kRedGroups) + threadIdx.x);
+    return;  // uniform over the block: no LDS used, the next logical block may follow at once
+  }
   if (blk < J.main_blocks) {
     const int64_t f = (int64_t)blk * kRedCols + col;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -629,10 +635,21 @@ bool add_reduce_job(RedJobs& jobs, const float* slab, const float* bslab, int sp
   J.Kout = Kout;
   J.gap_at = gap_at;
   J.gap_len = gap_len;
-  J.main_blocks = (int)cdiv(nf, kRedCols);
-  J.nblk = J.main_blocks + (bias_dst ? (int)cdiv(Nout, kRedCols) : 0);
+  red_job_set_splits(J, splits);
   jobs.total += J.nblk;
   return true;
+}
+
+void red_job_set_splits(RedJob& J, int splits) {
+  J.splits = splits;
+  const int64_t nf = (int64_t)J.Nout * (((J.Kout + 3) & ~3) >> 2);
+  if (splits < kRedGroups) {  // flat logical blocks (reduce_slab_block)
+    J.main_blocks = (int)cdiv(nf + (J.bias_dst ? J.Nout : 0), kRedCols * kRedGroups);
+    J.nblk = J.main_blocks;
+  } else {
+    J.main_blocks = (int)cdiv(nf, kRedCols);
+    J.nblk = J.main_blocks + (J.bias_dst ? (int)cdiv(J.Nout, kRedCols) : 0);
+  }
 }
 
 hipError_t reduce_slabs_batched(const RedJobs& jobs, int max_blocks, hipStream_t st) {

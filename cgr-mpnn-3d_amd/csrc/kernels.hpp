@@ -131,6 +131,8 @@ struct RedJobs {
 bool add_reduce_job(RedJobs& jobs, const float* slab, const float* bslab, int splits, int Nout,
                     int Kout, float* dst, int64_t ld_dst, int64_t col_off, float* bias_dst,
                     int gap_at = 0, int gap_len = 0);
+// set a job's split count and size its logical blocks for it (jobs made before their TN plan)
+void red_job_set_splits(RedJob& J, int splits);
 // grouped form grid (A/B: beats 64 and unbounded 4096 by 4-8 %)
 constexpr int kReduceMaxBlocks = 256;
 hipError_t reduce_slabs_batched(const RedJobs& jobs, int max_blocks, hipStream_t st);
