@@ -64,9 +64,13 @@ def parse():
     ap.add_argument("--infer-bench", type=int, default=1,
                     help="also measure the eval forward (SURVEY §8(f) rank 3), N=1 only")
     ap.add_argument("--cpu-baseline", type=int, default=1)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="per thread setting (the baseline runs at two)")
     ap.add_argument("--profile-steps", type=int, default=10,
                     help="instrumented steps (HIP events per kernel class) after the timed run")
+    ap.add_argument("--diag-blocks", type=int, default=0,
+                    help="diagnostic: time this many further blocks of --steps steps after the "
+                         "timed one (per-step HIP events); not part of `value`")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return ap.parse_args()
 
@@ -419,6 +423,40 @@ def host_cpu_info():
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
+def host_physical_cores():
+    """Physical cores this process may run on: the CPUs in its affinity mask scaled by the
+    machine's physical / logical ratio (SMT siblings are not extra cores)."""
+    info = host_cpu_info()
+    allowed = info["process_allowed_cpus"] or info["machine_logical_cpus"] or 1
+    phys, logical = info["machine_physical_cores"], info["machine_logical_cpus"]
+    if phys and logical:
+        return max(1, round(allowed * phys / logical))
+    return allowed
+
+
+def cpu_baseline_both(cfgname, seconds, dropout):
+    """the CPU baseline on the whole host (torch threads = the physical cores this
+    process may use) and, beside it, at the torch default (OMP_NUM_THREADS, 16 on the GPU boxes);
+    the line's `cpu_baseline` is the faster of the two, the other is kept under `alternative`."""
+    default_threads = torch.get_num_threads()
+    full = host_physical_cores()
+    runs = []
+    try:
+        for t in dict.fromkeys([full, default_threads]):
+            torch.set_num_threads(t)
+            runs.append(cpu_baseline(cfgname, seconds, dropout))
+    finally:
+        torch.set_num_threads(default_threads)
+    best = max(runs, key=lambda r: r["value"])
+    others = [r for r in runs if r is not best]
+    if others:
+        best = dict(best, alternative={k: others[0][k] for k in ("value", "cores", "sample")})
+    best["threads_rule"] = (f"timed at {full} threads (the physical cores this process may use) "
+                            f"and at the torch default {default_threads}; the faster is the "
+                            f"baseline")
+    return best
+
+
 def cpu_baseline(cfgname, seconds, dropout):
     """Reference CPU path (oracle/dmpnn_torch.py: the reference ATen op sequence incl. its dead
     readout GEMM) on this host's cores: same batch shape, MSE(sum) + backward + Adam(amsgrad)."""
@@ -464,8 +502,67 @@ def cpu_baseline(cfgname, seconds, dropout):
                       f"{torch.get_num_threads()} threads"}
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, cmd: list[str], env: dict | None = None, poll_s: float = 0.2) -> int:
+    """Run `cmd` as `n` fresh child processes, one per rank, with RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_ADDR (127.0.0.1) / MASTER_PORT set -- what `torch.distributed.run --nnodes=1
+    --nproc-per-node n` would set.  The caller must not have touched the GPU: the children are
+    started with subprocess (no exec), inherit stdout / stderr (rank 0's JSON line goes straight
+    through), and are waited for.  If one child fails, the others are terminated (then killed)
+    by PID so that a rank blocked in a collective does not hang the job.  Returns the first
+    non-zero exit status (negative = the signal a child died of), else 0."""
+    import subprocess
+
+    base = dict(os.environ if env is None else env)
+    base.setdefault("MASTER_ADDR", "127.0.0.1")
+    base.setdefault("MASTER_PORT", str(_free_port()))
+    base["WORLD_SIZE"] = str(n)
+    base["LOCAL_WORLD_SIZE"] = str(n)
+    base["CGR_BENCH_SPAWNED"] = "1"
+    procs = []
+    for r in range(n):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), GROUP_RANK="0")
+        procs.append(subprocess.Popen(cmd, env=e))
+    rc = 0
+    try:
+        while True:
+            alive = False
+            for r, p in enumerate(procs):
+                s = p.poll()
+                if s is None:
+                    alive = True
+                elif s != 0 and rc == 0:
+                    rc = s
+                    log(f"[bench] rank {r} exited with status {s}; stopping the other ranks")
+            if rc != 0 or not alive:
+                break
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    return rc
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no outside launcher: start the N ranks here, before anything touches the GPU
+        sys.exit(spawn_ranks(args.gpus, [sys.executable, "-u", os.path.abspath(__file__)]
+                             + sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -540,6 +637,7 @@ def main():
     g = None
     if args.graph and distributed and args.dist_backend != "nccl":
         args.graph = 0  # a gloo collective cannot be recorded into a HIP graph (host copies)
+    capture_note = None
     if args.graph:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
@@ -547,10 +645,28 @@ def main():
             for _ in range(3):
                 step()
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            step()
-        run = g.replay
+        ok = 1
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                step()
+        except Exception as exc:  # noqa: BLE001
+            # a capture the runtime refuses (e.g. a collective RCCL cannot record at this world
+            # size) must not end the scaling run: every rank then times the eager step
+            log(f"[bench] rank {rank}: step capture failed ({type(exc).__name__}: {exc}); "
+                f"timing the eager step")
+            g, ok = None, 0
+            torch.cuda.synchronize()
+        if world > 1:  # all ranks replay, or none does (a lone replayer would hang the others)
+            flag = torch.tensor([ok], device=dev, dtype=torch.int32)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            ok = int(flag.item())
+        if ok:
+            run = g.replay
+        else:
+            g = None
+            args.graph = 0
+            capture_note = "step capture failed on at least one rank; eager step timed"
         for _ in range(args.warmup):
             run()
         torch.cuda.synchronize()
@@ -573,6 +689,29 @@ def main():
         el = float(t.item())
     ms = el / args.steps * 1e3
     value = world * B * args.steps / el
+
+    diag = None
+    if args.diag_blocks > 0:
+        # more blocks of K steps straight after the timed one, each timed like
+        # it (host clock, device synchronised) plus a HIP event before every step on the launch
+        # stream -- whether the first K steps after a short warmup run slower than later ones
+        diag = []
+        stream = torch.cuda.current_stream(dev)
+        for _ in range(args.diag_blocks):
+            evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for i in range(args.steps):
+                evs[i].record(stream)
+                run()
+            evs[-1].record(stream)
+            torch.cuda.synchronize()
+            bl = time.perf_counter() - t1
+            st = [evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)]
+            diag.append({"ms_per_step": round(bl / args.steps * 1e3, 4),
+                         "event_ms_per_step": round(sum(st) / len(st), 4),
+                         "event_ms_first_last": [round(st[0], 4), round(st[-1], 4)],
+                         "event_ms_min_max": [round(min(st), 4), round(max(st), 4)]})
 
     # per-kernel-class device time with HIP events on the launch stream (eager, instrumented)
     lib = native.load()
@@ -663,7 +802,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         log("[bench] timing the CPU baseline (reference op sequence, torch CPU) ...")
-        cpu = cpu_baseline(args.config, args.cpu_seconds, args.dropout)
+        cpu = cpu_baseline_both(args.config, args.cpu_seconds, args.dropout)
 
     if rank == 0:
         out = {
@@ -692,6 +831,12 @@ def main():
             "roofline_frac_by_class": roof_all, "kernel_breakdown": breakdown,
             "cpu_baseline": cpu,
         }
+        if diag is not None:
+            out["diag_blocks"] = diag
+        if capture_note:
+            out["capture_note"] = capture_note
+        if os.environ.get("CGR_BENCH_SPAWNED") == "1":
+            out["launcher"] = "bench.py spawned its own ranks (no torch.distributed.run)"
         if coll is not None:
             out["collate"] = coll
         if infer is not None:
