@@ -37,6 +37,7 @@ class GradAllReduce:
         self.op = op
         self._streams = {}
         self._events = {}
+        self.captured = 0  # bucket collectives recorded into a stream capture (teardown checks)
 
     def bucket_events(self, dev, n):
         key = (dev.index if dev.index is not None else torch.cuda.current_device(), n)
@@ -74,6 +75,8 @@ class GradAllReduce:
         cs = self._streams.get(dev)
         if cs is None:
             cs = self._streams[dev] = torch.cuda.Stream(dev)
+        if torch.cuda.is_current_stream_capturing():
+            self.captured += len(buckets)
         for (a, b), ev in zip(buckets, events):
             cs.wait_event(ev)
             with torch.cuda.stream(cs):
@@ -95,7 +98,7 @@ def remove_grad_allreduce(model):
     return model
 
 
-def teardown(model=None):
+def teardown(model=None, graphs_released: bool = False):
     """End data parallelism in a fixed order that depends on no garbage collection, then destroy
     the process group.
 
@@ -114,11 +117,26 @@ def teardown(model=None):
     a collection at that point freed nothing of this process group's and only re-ordered the
     release of EARLIER work's objects against the communicator's own threads -- which is where
     the one round-4 abort struck (on a native thread, not in a destructor the
-    collector ran).  ``cgr_debug_abort_backtrace`` prints the native stack of any such abort."""
+    collector ran).  ``cgr_debug_abort_backtrace`` prints the native stack of any such abort.
+
+    ``graphs_released``: the caller's statement that step (1) is done.  When the model's hook
+    recorded collectives into a capture and the caller does not say so, a RuntimeWarning names
+    the precondition before the communicator is destroyed (no live graph can be enumerated from
+    here: torch keeps no registry of CUDAGraph objects)."""
     import gc
 
     if not dist.is_initialized():
         return
+    hook = getattr(model, "_grad_bucket_hook", None) if model is not None else None
+    if getattr(hook, "captured", 0) and not graphs_released:
+        import warnings
+
+        warnings.warn(
+            "ddp.teardown: the gradient hook recorded RCCL collectives into a captured graph; "
+            "drop every such graph (and any bound g.replay) before teardown and pass "
+            "graphs_released=True -- a captured collective's graph destroyed after the "
+            "communicator releases its RCCL state against a freed communicator", RuntimeWarning,
+            stacklevel=2)
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     if model is not None:

@@ -59,6 +59,7 @@ class ArenaRun:
         ws = torch.empty(lib.cgr_gnn_workspace_bytes(ctypes.byref(self.cfg), self.N, self.E,
                                                      self.B), dtype=torch.uint8, device=dev)
         grads = [torch.empty_like(p) for p in params]
+        self.ws = ws
         with native.device_guard(dev):
             native.check(lib.cgr_gnn_backward(
                 ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
@@ -66,3 +67,18 @@ class ArenaRun:
                 self.flags, native.ptr(self.arena), native.ptr(dy.contiguous()),
                 _param_table(grads), native.ptr(ws), None, native.stream_ptr(dev)))
         return grads
+
+    def input_grads(self, dy, params, ws):
+        """cgr_gnn_input_grads on this arena with workspace `ws` -> (dx, dedge_attr)."""
+        lib = native.load()
+        dev = dy.device
+        F_ = self.cfg.num_node_features
+        Fe = self.cfg.num_edge_features
+        dx = torch.empty(self.N, F_, device=dev)
+        de = torch.empty(self.E, Fe, device=dev) if Fe else None
+        with native.device_guard(dev):
+            native.check(lib.cgr_gnn_input_grads(
+                ctypes.byref(self.cfg), _param_table(params), ctypes.byref(self.bs),
+                native.ptr(self.arena), native.ptr(dy.contiguous()), native.ptr(ws),
+                native.ptr(dx), native.ptr(de), native.stream_ptr(dev)))
+        return dx, de

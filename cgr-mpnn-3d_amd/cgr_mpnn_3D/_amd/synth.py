@@ -176,6 +176,42 @@ def make_batch(num_graphs: int, n_atoms: int = 30, n_bonds: int = 30, n_mace: in
     )
 
 
+def make_symmetric_batch(num_graphs: int, n_leaves: int = 3, n_chain: int = 6, n_mace: int = 8,
+                         seed: int = 1234) -> RxnBatch:
+    """Batch of reactions with symmetric atoms (the explicit hydrogens of one carbon): atom 0
+    carries ``n_leaves`` identical leaf atoms (same features, same bond features), then a chain
+    of ``n_chain`` atoms.  Every value the model computes for the leaves is then identical, so a
+    ``global_max_pool`` column that a leaf wins is a tie (the tie-sharing gradient case)."""
+    rng = np.random.default_rng(seed)
+    L = n_leaves
+    A = 1 + L + n_chain
+    pairs = [(0, i) for i in range(1, L + 1)] + [(0, L + 1)] + \
+        [(L + 1 + j, L + 2 + j) for j in range(n_chain - 1)]
+    P = len(pairs)
+    xs, eis, eas, bs, ptr, off = [], [], [], [], [0], 0
+    for g in range(num_graphs):
+        x, _, ea = _one_reaction(rng, A, A - 1, n_mace)
+        assert ea.shape[0] == 2 * P
+        x[2:L + 1] = x[1]
+        for k in range(1, L):
+            ea[2 * k:2 * k + 2] = ea[0:2]
+        pa = np.asarray(pairs, dtype=np.int64)
+        ei = np.empty((2, 2 * P), dtype=np.int64)
+        ei[0, 0::2], ei[1, 0::2] = pa[:, 0], pa[:, 1]
+        ei[0, 1::2], ei[1, 1::2] = pa[:, 1], pa[:, 0]
+        xs.append(x)
+        eis.append(ei + off)
+        eas.append(ea)
+        bs.append(np.full(A, g, dtype=np.int64))
+        off += A
+        ptr.append(off)
+    y = (80.0 + 20.0 * rng.standard_normal(num_graphs)).astype(np.float32)
+    return RxnBatch(x=np.ascontiguousarray(np.concatenate(xs, 0)),
+                    edge_index=np.ascontiguousarray(np.concatenate(eis, 1)),
+                    edge_attr=np.ascontiguousarray(np.concatenate(eas, 0)),
+                    batch=np.concatenate(bs, 0), ptr=np.asarray(ptr, dtype=np.int64), y=y)
+
+
 # Named workloads of BASELINE.json "configs" (SURVEY.md §8d).
 CONFIGS = {
     "cfg1": dict(num_graphs=32, n_atoms=30, n_bonds=30, n_mace=0, depth=2, hidden=128,

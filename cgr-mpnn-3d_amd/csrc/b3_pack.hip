@@ -184,10 +184,12 @@ __global__ __launch_bounds__(256) void k_b3_segsum_eimage(const float* __restric
   float4 acc[2], x0[2], x1[2], x2[2];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
-    const int last = e[h] > b[h] ? e[h] - 1 : 0;  // clamped: always a valid entry (R >= 1)
-    x0[h] = ld(min(b[h], last));
-    x1[h] = ld(min(b[h] + 1, last));
-    x2[h] = ld(min(b[h] + 2, last));
+    // clamped into the segment; an empty segment loads nothing (idx may have no entries)
+    const bool any = e[h] > b[h];
+    const int last = any ? e[h] - 1 : 0;
+    x0[h] = any ? ld(min(b[h], last)) : f4zero();
+    x1[h] = any ? ld(min(b[h] + 1, last)) : f4zero();
+    x2[h] = any ? ld(min(b[h] + 2, last)) : f4zero();
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -268,7 +270,8 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
     const float* __restrict__ dy, const float* __restrict__ wf, const int* __restrict__ node_graph,
     const float* __restrict__ hn, const float* __restrict__ zn, int64_t N, int H, int Hp, int act,
     float* __restrict__ dzn, int colblocks, int cimg, b3_u4* __restrict__ img,
-    const float* __restrict__ gscale, const int* __restrict__ pool_arg) {
+    const float* __restrict__ gscale, const int* __restrict__ pool_arg,
+    const float* __restrict__ gpool) {
   __shared__ float tile[32][kImgCols + 1];
   const int64_t s = blockIdx.x / colblocks;
   const int c0 = (int)(blockIdx.x - s * colblocks) * kImgCols;
@@ -285,12 +288,19 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
       o.y = d * wf[min(n + 1, H - 1)];
       o.z = d * wf[min(n + 2, H - 1)];
       o.w = d * wf[min(n + 3, H - 1)];
-      if (pool_arg) {  // global_max_pool: the gradient of a column goes to its arg-max node
+      if (pool_arg) {  // global_max_pool (pool_head_fwd's record, kernels.hpp)
         const int4 am = *reinterpret_cast<const int4*>(pool_arg + (int64_t)gv * Hp + n);
-        o.x = am.x == v ? o.x : 0.f;
-        o.y = am.y == v ? o.y : 0.f;
-        o.z = am.z == v ? o.z : 0.f;
-        o.w = am.w == v ? o.w : 0.f;
+        const float4 h = *reinterpret_cast<const float4*>(hn + off);
+        const float4 gm = *reinterpret_cast<const float4*>(gpool + (int64_t)gv * Hp + n);
+        // the first arg-max node (>= 0), or every node holding the max sharing (-count)
+        auto pick = [&](float ov, int a, float hv, float gmv) {
+          if (a >= 0) return a == v ? ov : 0.f;
+          return hv == gmv ? ov / (float)(-a) : 0.f;
+        };
+        o.x = pick(o.x, am.x, h.x, gm.x);
+        o.y = pick(o.y, am.y, h.y, gm.y);
+        o.z = pick(o.z, am.z, h.z, gm.z);
+        o.w = pick(o.w, am.w, h.w, gm.w);
       }
       if (act == ACT_RELU) {
         const float4 h = *reinterpret_cast<const float4*>(hn + off);
@@ -317,13 +327,13 @@ __global__ __launch_bounds__(256) void k_readout_bwd_img(
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
                            float* dzn, void* img, hipStream_t st, const float* gscale,
-                           const int* pool_arg) {
+                           const int* pool_arg, const float* gpool) {
   if (N <= 0 || (!dzn && !img)) return hipSuccess;
   const int colblocks = (int)cdiv(Hp, kImgCols);
   const int64_t blocks = cdiv(N, 32) * colblocks;
   hipLaunchKernelGGL(k_readout_bwd_img, dim3((unsigned)blocks), dim3(256), 0, st, dy, wf,
                      node_graph, hn, zn, N, H, Hp, act, dzn, colblocks, b3_eimg_cols(H),
-                     static_cast<b3_u4*>(img), gscale, pool_arg);
+                     static_cast<b3_u4*>(img), gscale, pool_arg, gpool);
   return hipGetLastError();
 }
 

@@ -23,14 +23,32 @@ void set_error(const std::string& msg) { g_err = msg; }
 // them, so the table stays as small as the set of live arena blocks.
 static std::mutex g_arena_mu;
 static std::unordered_map<const void*, int> g_arena_flags;
+// every forward into an arena starts a new generation of it; a backward enqueued on (arena,
+// generation) records its workspace, and cgr_gnn_input_grads -- which reads dpre0 and the
+// readout's operands from that workspace -- requires the record to name the same arena at its
+// current generation (otherwise it silently returned garbage)
+static std::unordered_map<const void*, uint64_t> g_arena_gen;
+static std::unordered_map<const void*, std::pair<const void*, uint64_t>> g_ws_backward;
 static void note_forward(const void* arena, int flags) {
   std::lock_guard<std::mutex> lk(g_arena_mu);
   g_arena_flags[arena] = flags;
+  ++g_arena_gen[arena];
 }
 static int forward_flags(const void* arena) {
   std::lock_guard<std::mutex> lk(g_arena_mu);
   const auto it = g_arena_flags.find(arena);
   return it == g_arena_flags.end() ? -1 : it->second;
+}
+static void note_backward(const void* arena, const void* workspace) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  g_ws_backward[workspace] = {arena, g_arena_gen[arena]};
+}
+static bool backward_matches(const void* arena, const void* workspace) {
+  std::lock_guard<std::mutex> lk(g_arena_mu);
+  const auto it = g_ws_backward.find(workspace);
+  if (it == g_ws_backward.end() || it->second.first != arena) return false;
+  const auto g = g_arena_gen.find(arena);
+  return g != g_arena_gen.end() && g->second == it->second.second;
 }
 
 int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch* b,
@@ -476,9 +494,11 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params, cons
   if (bucket_events)
     for (int i = 0; i < CGR_GRAD_BUCKETS(cfg->depth); ++i)
       CGR_CHECK(bucket_events[i] != nullptr, "cgr_gnn_backward: NULL bucket event");
-  return gnn_backward_impl(d, params, b, dropout_p, seed, training, arena, dy, grads, workspace,
-                           reinterpret_cast<hipEvent_t const*>(bucket_events),
-                           (hipStream_t)stream);
+  const int r = gnn_backward_impl(d, params, b, dropout_p, seed, training, arena, dy, grads,
+                                  workspace, reinterpret_cast<hipEvent_t const*>(bucket_events),
+                                  (hipStream_t)stream);
+  if (r == 0) note_backward(arena, workspace);
+  return r;
 }
 
 int cgr_gnn_input_grads(const cgr_gnn_config* cfg, const float* const* params,
@@ -495,6 +515,9 @@ int cgr_gnn_input_grads(const cgr_gnn_config* cfg, const float* const* params,
   CGR_CHECK(ff >= 0 && (ff & CGR_TRAIN_FOR_BACKWARD),
             "cgr_gnn_input_grads: `arena` was not filled by a successful cgr_gnn_forward with "
             "CGR_TRAIN_FOR_BACKWARD set");
+  CGR_CHECK(backward_matches(arena, workspace),
+            "cgr_gnn_input_grads: `workspace` does not hold a cgr_gnn_backward of this `arena`'s "
+            "latest forward (run the backward first, with the same arena and workspace)");
   CGR_CHECK(((uintptr_t)dx & 15) == 0 && ((uintptr_t)dedge_attr & 15) == 0,
             "cgr_gnn_input_grads: dx / dedge_attr must be 16-byte aligned (or NULL)");
   const int np = cgr_gnn_num_params(cfg);

@@ -309,7 +309,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
   if (max_pool) {  // dzn (fp32 for the NT, and the TN's e-image) before the fork
     ProfScope _p("readout_act_bwd", st);
     HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H, Hp,
-                            d.act, dzn, ro_b3 ? img_side : nullptr, st, nullptr, fv.pool_arg));
+                            d.act, dzn, ro_b3 ? img_side : nullptr, st, nullptr, fv.pool_arg, fv.g));
   }
   if (side != st) HIP_RET(fork_to(ss, st, side));
   if (const int rc = side_readout()) return rc;
@@ -586,7 +586,7 @@ int gnn_input_grads_impl(const Dims& d, const float* const* params, const void* 
       ProfScope _p("input_grad_prep", st);
       HIP_RET(segment_sum(dpre0, Hp, iv.src_list, iv.src_ptr, N, H, Gs, Hp, st));
       HIP_RET(readout_act_bwd(dy, params[CGR_PARAM_FFN_W(D)], iv.node_graph, fv.hn, fv.zn, N, H,
-                              Hp, d.act, dzn, nullptr, st, fv.inv_cnt, fv.pool_arg));
+                              Hp, d.act, dzn, nullptr, st, fv.inv_cnt, fv.pool_arg, fv.g));
       TransposeJobs tj{};  // wxT [F, ldw] = [W0[:, :F]^T | W_n[:, :F]^T]
       tj.job[0] = TransposeJob{params[CGR_PARAM_EDGE_INIT_W], F + Fe, 0, wxT, ldw, H, F};
       tj.job[1] = TransposeJob{params[CGR_PARAM_E2N_W(D)], F + H, 0, wxT + H, ldw, H, F};

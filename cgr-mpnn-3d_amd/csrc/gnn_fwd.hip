@@ -340,7 +340,8 @@ int gnn_forward_impl(const Dims& d, const float* const* params, const cgr_batch*
   }
   ProfScope _p("pool_head_fwd", st);
   HIP_RET(pool_head_fwd(fv.hn, Hp, iv.graph_ptr, d.B, H, params[CGR_PARAM_FFN_W(D)],
-                        params[CGR_PARAM_FFN_B(D)], fv.g, y, st, fv.inv_cnt, fv.pool_arg));
+                        params[CGR_PARAM_FFN_B(D)], fv.g, y, st, fv.inv_cnt, fv.pool_arg,
+                        b->batch == nullptr));
   return 0;
 }
 

@@ -48,9 +48,9 @@ __global__ __launch_bounds__(256) void k_segsum_v4m(const float* __restrict__ va
     const int last = e[k] > b[k] ? e[k] - 1 : b[k];
     const float* base = vals + 4 * c[k];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int jj = min(b[k] + j, last);
-      x[k][j] = *reinterpret_cast<const float4*>(base + (e[k] > b[k] ? row(jj) : 0) * ldv);
+    for (int j = 0; j < 3; ++j) {  // an empty segment (or a thread past the end) loads nothing:
+      const int jj = min(b[k] + j, last);  // `vals` may have no rows at all
+      x[k][j] = e[k] > b[k] ? *reinterpret_cast<const float4*>(base + row(jj) * ldv) : f4zero();
     }
   }
 #pragma unroll
@@ -343,7 +343,8 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
                                                             float* __restrict__ g,
                                                             float* __restrict__ y,
                                                             const float* __restrict__ inv_cnt,
-                                                            int* __restrict__ pool_arg) {
+                                                            int* __restrict__ pool_arg,
+                                                            bool pool_first) {
   const int b = blockIdx.x;
   const int v0 = gptr[b], v1 = gptr[b + 1];
   const int C4 = Hp >> 2;
@@ -352,9 +353,9 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
   for (int c = threadIdx.x; c < C4; c += kPoolThreads) {
     const float* col = hn + 4 * c;
     float4 s = f4zero();
-    if (pool_arg) {  // global_max_pool: the largest value, its first node (empty graph: 0, -1)
+    if (pool_arg) {  // global_max_pool: the largest value, its first node and its tie count
       float m[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      int arg[4] = {-1, -1, -1, -1};
+      int arg[4] = {-1, -1, -1, -1}, cnt[4] = {0, 0, 0, 0};
       for (int v = v0; v < v1; ++v) {
         const float4 x = *reinterpret_cast<const float4*>(col + (int64_t)v * Hp);
         const float xv[4] = {x.x, x.y, x.z, x.w};
@@ -363,12 +364,19 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
           if (xv[k] > m[k] || arg[k] < 0) {
             m[k] = xv[k];
             arg[k] = v;
+            cnt[k] = 1;
+          } else if (xv[k] == m[k]) {
+            ++cnt[k];
           }
       }
-      if (v1 <= v0) m[0] = m[1] = m[2] = m[3] = 0.f;
+      if (v1 <= v0) m[0] = m[1] = m[2] = m[3] = 0.f;  // (empty graph: 0, entry -1, never read)
       s = make_float4(m[0], m[1], m[2], m[3]);
+      int rec[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k)  // torch's amax backward also counts the zero `self` at a 0 max
+        rec[k] = pool_first || arg[k] < 0 ? arg[k] : -(cnt[k] + (m[k] == 0.f ? 1 : 0));
       *reinterpret_cast<int4*>(pool_arg + (int64_t)b * Hp + 4 * c) =
-          make_int4(arg[0], arg[1], arg[2], arg[3]);
+          make_int4(rec[0], rec[1], rec[2], rec[3]);
     } else {
       for (int v = v0; v < v1; v += kPoolBatch) {
         float4 x[kPoolBatch];
@@ -403,10 +411,10 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool_head(const float* __restr
 
 hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
                          const float* wf, const float* bf, float* g, float* y, hipStream_t st,
-                         const float* inv_cnt, int* pool_arg) {
+                         const float* inv_cnt, int* pool_arg, bool pool_first) {
   if (B <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_pool_head, dim3(B), dim3(kPoolThreads), 0, st, hn, Hp, gptr, H, wf, bf, g,
-                     y, inv_cnt, pool_arg);
+                     y, inv_cnt, pool_arg, pool_first);
   return hipGetLastError();
 }
 

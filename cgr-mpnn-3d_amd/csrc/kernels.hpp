@@ -46,10 +46,14 @@ hipError_t edge_init_fwd(const float* P, const int* src_s, const float* e_s, int
                          float* h0, float* pre0, hipStream_t st);
 
 // g[b] = sum_{v in graph b} hn[v] (* inv_cnt[b]: mean pooling, nullable; pool_arg non-null:
-// max pooling, per column the max and its first node into pool_arg [B, Hp]);  y[b] = g[b].wf + bf
+// max pooling, per column the max into g and into pool_arg [B, Hp] what its gradient needs:
+// pool_first (batch=None: PyG's x.max(dim=-2), torch.max's first index) the first arg-max node,
+// else (scatter_reduce "amax", include_self=False) -count, count = the nodes holding the max plus
+// one when the max is 0 (the zero `self` torch's backward also counts));  y[b] = g[b].wf + bf
 hipError_t pool_head_fwd(const float* hn, int Hp, const int* gptr, int64_t B, int H,
                          const float* wf, const float* bf, float* g, float* y, hipStream_t st,
-                         const float* inv_cnt = nullptr, int* pool_arg = nullptr);
+                         const float* inv_cnt = nullptr, int* pool_arg = nullptr,
+                         bool pool_first = false);
 
 // mean aggregation / pooling factors: inv_deg[v] = 1 / max(in-degree, 1) from the dst CSR,
 // inv_cnt[b] = 1 / max(nodes of graph b, 1) (either nullable: not computed)
@@ -65,11 +69,13 @@ hipError_t head_bwd(const float* dy, const float* g, const float* wf, int64_t B,
 // dzn[v] = dy[graph(v)] * wf * act'(zn[v])   (ReLU: hn > 0)
 // dzn (may be null: not materialised) and/or its e-image `img` (gemm_b3.hpp B3EImg; null: none)
 // gscale (nullable): per-graph factor of dy (mean pooling: inv_cnt); pool_arg (nullable): max
-// pooling, dzn[v, n] kept only where v is the graph's arg-max node of column n
+// pooling (pool_head_fwd's record): dzn[v, n] kept only where v is the column's first arg-max node
+// (entry >= 0) or, for an entry -count, where hn[v, n] equals the pooled g[graph(v), n], divided
+// by count (torch's scatter_reduce amax backward: ties share the gradient)
 hipError_t readout_act_bwd(const float* dy, const float* wf, const int* node_graph,
                            const float* hn, const float* zn, int64_t N, int H, int Hp, int act,
                            float* dzn, void* img, hipStream_t st, const float* gscale = nullptr,
-                           const int* pool_arg = nullptr);
+                           const int* pool_arg = nullptr, const float* gpool = nullptr);
 
 struct LayerBwdArgs {
   // dh_{l+1}: top layer (l == D-1, layer_act_bwd): ds[dst_s[i]]; below (the fused dm GEMM,

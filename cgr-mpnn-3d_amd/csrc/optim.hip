@@ -3,7 +3,9 @@
 // (amsgrad), float4 when every pointer of a tensor is 16-byte aligned, scalar otherwise.
 #include <math.h>
 
+#include "common.hpp"
 #include "gnn_internal.hpp"
+#include "streams.hpp"
 
 namespace cgr {
 
@@ -18,6 +20,10 @@ struct AdamGroup {
   int32_t vec4[CGR_ADAM_GROUP];
   int32_t first_block[CGR_ADAM_GROUP + 1];
   int32_t n;
+  // the timeout gate (streams.hpp adam_gate): `err` = the host-mapped error words, `gate` = the
+  // device word the step-count kernel sets from them; both null = ungated
+  const int* err;
+  int* gate;
 };
 
 struct AdamHyper {
@@ -32,10 +38,20 @@ constexpr int kAdamThreads = 256;
 // replayed step for 54 MB)
 constexpr int kAdamElemsPerBlock = kAdamThreads * 4;
 
-// t <- t + 1 for every tensor of the group (before k_adam reads it, same stream)
+// t <- t + 1 for every tensor of the group (before k_adam reads it, same stream) -- unless an
+// unpaired backward's completion timed out (its gradients are NaN): then the gate word tells
+// k_adam to skip the step, and the parameters stay finite until the model's next forward raises
 __global__ void k_adam_step_count(AdamGroup G) {
+  __shared__ int poisoned;
+  if (threadIdx.x == 0) {
+    poisoned = G.err ? __hip_atomic_load(G.err + kDevErrUnpairedTimeout, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) != 0
+                     : 0;
+    if (G.gate) G.gate[0] = poisoned;
+  }
+  __syncthreads();
   const int i = threadIdx.x;
-  if (i < G.n) G.step[i][0] = G.step[i][0] + 1.f;
+  if (i < G.n && !poisoned) G.step[i][0] = G.step[i][0] + 1.f;
 }
 
 // torch _multi_tensor_adam order: lerp_ (weight < 0.5: m + w (g - m)), mul_(b2), addcmul_,
@@ -57,6 +73,7 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
 }
 
 __global__ __launch_bounds__(kAdamThreads) void k_adam(AdamGroup G, AdamHyper h) {
+  if (G.gate && G.gate[0]) return;  // the gradients are NaN-poisoned: no update (above)
   const int b = blockIdx.x;
   int t = 0;
   while (t + 1 < G.n && G.first_block[t + 1] <= b) ++t;
@@ -123,7 +140,14 @@ extern "C" int cgr_adam_step(const cgr_adam_tensor* tensors, int32_t num_tensors
                     (float)weight_decay,
                     amsgrad ? 1 : 0,
                     maximize ? 1 : 0};
+  int dev = -1;
+  SideStreams* ss = hipStreamGetDevice(st, &dev) == hipSuccess ? side_streams_of(dev) : nullptr;
+  (void)hipGetLastError();
+  const int* err = ss && ss->adam_gate ? ss->dev_err : nullptr;
+  int* gate = ss ? ss->adam_gate : nullptr;
   AdamGroup G{};
+  G.err = err;
+  G.gate = gate;
   auto flush = [&]() -> int {
     if (G.n == 0) return 0;
     const int blocks = G.first_block[G.n];
@@ -134,6 +158,8 @@ extern "C" int cgr_adam_step(const cgr_adam_tensor* tensors, int32_t num_tensors
       HIP_RET(hipGetLastError());
     }
     G = AdamGroup{};
+    G.err = err;
+    G.gate = gate;
     return 0;
   };
   for (int i = 0; i < num_tensors; ++i) {

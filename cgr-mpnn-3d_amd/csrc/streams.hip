@@ -106,6 +106,12 @@ SideStreams* side_streams(hipStream_t main) {
       (void)hipHostFree(h);
     }
   }
+  s->adam_gate = nullptr;
+  if (s->dev_err) {
+    void* g = nullptr;
+    if (hipMalloc(&g, 64) == hipSuccess && hipMemset(g, 0, 64) == hipSuccess)
+      s->adam_gate = static_cast<int*>(g);
+  }
   (void)hipGetLastError();  // a failed pinned allocation only disables the error words
   g_side[dev] = s;
   return s;

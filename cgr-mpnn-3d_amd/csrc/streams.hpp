@@ -23,6 +23,10 @@ struct SideStreams {
   // (cgr_device_errors); null if the pinned allocation failed
   int* err_host;
   int* dev_err;
+  // device word written by the fused Adam's step-count kernel: 1 when the error words hold an
+  // unpaired-backward timeout (the step's gradients are NaN-poisoned), and k_adam then leaves
+  // every parameter and state untouched (optim.hip); null if the allocation failed
+  int* adam_gate;
 };
 
 // CGR_SINGLE_STREAM=1 in the environment: everything on the caller's stream (A/B of the

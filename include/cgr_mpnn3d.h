@@ -60,8 +60,10 @@ typedef struct cgr_gnn_config {
  * (the sum over a node's in-edges divided by their count, 0 for a node without in-edges) */
 enum cgr_aggregation { CGR_AGGR_ADD = 0, CGR_AGGR_MEAN = 1 };
 /* pooling_fn: global_add_pool (default), global_mean_pool (the graph's node sum divided by its
- * node count) or global_max_pool (per column the largest node value; its gradient goes to the
- * first node holding it) */
+ * node count) or global_max_pool (per column the largest node value; with a `batch` its gradient
+ * is shared evenly by the nodes holding it, as torch's scatter_reduce("amax", include_self=False)
+ * backward does -- the zero `self` counted when the max is 0; with batch == NULL, x.max(dim=-2),
+ * it goes to the first node holding it) */
 enum cgr_pooling { CGR_POOL_ADD = 0, CGR_POOL_MEAN = 1, CGR_POOL_MAX = 2 };
 
 /* One collated batch, the fields GNN.forward reads from a PyG Batch (GNN.py:77-82). */
@@ -166,7 +168,8 @@ int cgr_gnn_backward(const cgr_gnn_config* cfg, const float* const* params,
  * the SAME workspace (it reads the edge-init pre-activation gradient that backward left there).
  * dx: device [num_nodes, num_node_features] (NULL: skipped); dedge_attr: device
  * [num_edges, num_edge_features] in the caller's edge order (NULL: skipped); both overwritten,
- * fp32, 16-byte aligned. */
+ * fp32, 16-byte aligned.  Fails (nothing enqueued) unless `workspace` holds a successful
+ * cgr_gnn_backward of `arena`'s latest forward (host-side record, no device sync). */
 int cgr_gnn_input_grads(const cgr_gnn_config* cfg, const float* const* params,
                         const cgr_batch* batch, const void* arena, const float* dy,
                         void* workspace, float* dx, float* dedge_attr, void* stream);

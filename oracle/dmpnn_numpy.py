@@ -122,9 +122,12 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
     ``aggr`` ("add" / "mean"): DMPNNConv's PyG aggregation (GNN.py:22,63,119); ``pool`` ("add" /
     "mean" / "max"): global_add_pool / global_mean_pool / global_max_pool (GNN.py:23,110).  PyG's
     mean is the sum divided by max(count, 1) (torch_geometric.utils.scatter, reduce="mean"), its
-    max a column-wise amax whose gradient this restatement gives to the first arg-max node
-    (PyG is absent here, its semantics restated; ties do not occur on continuous data except at
-    ReLU's exact zeros, whose gradient the activation zeroes anyway).
+    max a column-wise amax: with a ``batch`` PyG runs ``scatter_reduce_(..., "amax",
+    include_self=False)`` into zeros, whose backward shares a column's gradient evenly over the
+    nodes holding the max and also counts the zero ``self`` when the max is 0 (torch
+    FunctionsManual scatter_reduce_backward; checked against torch in tests/test_oracle_golden.py);
+    with ``batch=None`` it is ``x.max(dim=-2)``, whose gradient goes to the first arg-max node.
+    (PyG is absent here, its semantics restated.)
 
     ``params`` uses the reference ``state_dict`` keys.  ``dropout_masks[l]`` (optional, 0/1 per
     element of h) + ``dropout_ps[l]`` reproduce ``F.dropout`` in train mode with a given mask.
@@ -194,10 +197,11 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
         g = _scatter_sum(hnode, gid, B)  # GNN.py:110 global_add_pool
     inv_cnt = np.ones(B)
     pool_arg = None
+    pool_share = None  # [N, H] each node's share of its column's gradient (max pool, batched)
     if pool == "mean":  # global_mean_pool
         inv_cnt = 1.0 / np.maximum(np.bincount(gid, minlength=B)[:B], 1)
         g = g * inv_cnt[:, None]
-    elif pool == "max":  # global_max_pool: column max per graph, the gradient to its first node
+    elif pool == "max":  # global_max_pool: column max per graph
         g = np.zeros((B, hnode.shape[1]))
         pool_arg = np.full((B, hnode.shape[1]), -1, dtype=np.int64)
         for b in range(B):
@@ -206,6 +210,12 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
                 k = np.argmax(hnode[nodes], axis=0)  # first occurrence of the max
                 pool_arg[b] = nodes[k]
                 g[b] = hnode[nodes[k], np.arange(hnode.shape[1])]
+        if batch is not None:  # scatter_reduce amax: ties share, the zero `self` counts at 0
+            eq = hnode == g[gid]
+            cnt = np.zeros((B, hnode.shape[1]))
+            np.add.at(cnt, gid, eq.astype(np.float64))
+            cnt = cnt + (g == 0.0)
+            pool_share = np.where(eq, 1.0 / np.maximum(cnt[gid], 1.0), 0.0)
     wf = np.asarray(params["ffn.weight"], f8)  # [1, H]
     bf = np.asarray(params["ffn.bias"], f8)
     y = (g @ wf.T + bf)[:, 0]
@@ -213,7 +223,7 @@ def forward(params: dict, x, edge_index, edge_attr, batch, depth: int, act: str 
                  zs=zs, s=s, qn=qn, zn=zn, hnode=hnode, g=g, gid=gid, B=B, sig=sig, N=N, E=E,
                  depth=depth, act=act, learnable_skip=learnable_skip,
                  masks=dropout_masks, ps=dropout_ps, relu_masks=rm, inv_deg=inv_deg,
-                 inv_cnt=inv_cnt, pool_arg=pool_arg)
+                 inv_cnt=inv_cnt, pool_arg=pool_arg, pool_share=pool_share)
     return y, cache
 
 
@@ -242,7 +252,9 @@ def backward(params: dict, cache: dict, dy: np.ndarray, inputs_out: dict | None 
 
     inv_deg, inv_cnt = cache["inv_deg"], cache["inv_cnt"]
     dhnode = (dg * inv_cnt[:, None])[cache["gid"]]  # pooling backward = gather by graph id
-    if cache.get("pool_arg") is not None:  # max pooling: only each column's arg-max node
+    if cache.get("pool_share") is not None:  # max pooling (batched): ties share the gradient
+        dhnode = dhnode * cache["pool_share"]
+    elif cache.get("pool_arg") is not None:  # max pooling, batch=None: the first arg-max node
         dhnode = dhnode * (cache["pool_arg"][cache["gid"]] == np.arange(N)[:, None])
     dzn = dhnode * grad_of(cache["zn"], "zn")
     grads["edge_to_node.weight"] = dzn.T @ cache["qn"]

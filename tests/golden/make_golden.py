@@ -35,7 +35,7 @@ import torch.nn.functional as F
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "cgr-mpnn-3d_amd"))
-from cgr_mpnn_3D._amd.synth import make_batch  # noqa: E402
+from cgr_mpnn_3D._amd.synth import make_batch, make_symmetric_batch  # noqa: E402
 
 REF_GNN = "/root/reference/cgr_mpnn_3D/models/GNN.py"
 
@@ -163,11 +163,24 @@ CASES = {
     "max_pool_silu": (dict(num_graphs=5, n_atoms=16, n_bonds=18, n_mace=8, seed=23,
                            n_atoms_jitter=6),
                       dict(depth=3, hidden=32, act="silu", skip=False), {"pool": "max"}),
+    # global_max_pool over symmetric atoms (identical leaves on one atom): columns a leaf wins are
+    # ties, whose gradient scatter_reduce("amax") shares evenly
+    "max_pool_ties_silu": (dict(num_graphs=4, n_leaves=3, n_chain=6, n_mace=8, seed=24,
+                                symmetric=True),
+                           dict(depth=2, hidden=32, act="silu", skip=False), {"pool": "max"}),
+    # the same with batch=None: x.max(dim=-2), whose gradient goes to the first arg-max only
+    "max_pool_ties_none": (dict(num_graphs=1, n_leaves=3, n_chain=5, n_mace=8, seed=25,
+                                symmetric=True),
+                           dict(depth=2, hidden=24, act="gelu", skip=False),
+                           {"pool": "max", "batch_none": True}),
 }
 
 
 def run_case(ref, name, bkw, mkw, extra):
-    b = make_batch(**bkw)
+    if bkw.get("symmetric"):
+        b = make_symmetric_batch(**{k: v for k, v in bkw.items() if k != "symmetric"})
+    else:
+        b = make_batch(**bkw)
     x = torch.from_numpy(b.x)
     ei = torch.from_numpy(b.edge_index)
     ea = torch.from_numpy(b.edge_attr)

@@ -134,3 +134,27 @@ def test_sum_allreduce_of_shard_gradients_equals_global_batch_gradient():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert err < 1e-12
+
+
+def test_teardown_warns_when_captured_collectives_may_outlive_the_group():
+    """ddp.teardown's precondition (drop every graph that recorded a collective first) is a
+    checked argument: a hook that recorded collectives into a capture, torn down without
+    graphs_released=True, warns before the communicator is destroyed."""
+    import warnings
+
+    from cgr_mpnn_3D._amd.ddp import teardown
+
+    class _M:
+        pass
+
+    for released, expect in ((False, True), (True, False)):
+        store = dist.TCPStore("127.0.0.1", _free_port(), 1, True)
+        dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+        m = install_grad_allreduce(_M())
+        m._grad_bucket_hook.captured = 3  # as after a captured backward
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            teardown(m, graphs_released=released)
+        hits = [x for x in w if "graphs_released" in str(x.message)]
+        assert bool(hits) == expect
+        assert not dist.is_initialized() and m._grad_bucket_hook is None

@@ -132,7 +132,8 @@ def _rccl_world1_child():
     eager = _grads(m, data)
     cap = _captured(m, data)  # its graph (with the captured collectives) is gone on return
     ok = all(torch.equal(a, r) and torch.equal(c, r) for a, c, r in zip(eager, cap, ref))
-    teardown(m)
+    assert m._grad_bucket_hook.captured > 0  # the hook knows it recorded collectives
+    teardown(m, graphs_released=True)
     assert not dist.is_initialized() and m._grad_bucket_hook is None
     print(f"RCCL_WORLD1_BITWISE={ok}", flush=True)
 

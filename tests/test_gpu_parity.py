@@ -17,6 +17,7 @@ from conftest import golden_cases, load_golden
 
 from cgr_mpnn_3D._amd import native
 from cgr_mpnn_3D._amd.debug import ArenaRun
+from cgr_mpnn_3D._amd.optim import FusedAdam
 from cgr_mpnn_3D._amd.synth import TorchBatch, make_batch
 from cgr_mpnn_3D.models.GNN import GNN
 from oracle import dmpnn_numpy as on
@@ -154,6 +155,35 @@ def test_input_gradients_only_x_and_frozen_parameters(cuda_device):
     assert data.edge_attr.grad is None
     assert_g_close(data.x.grad.cpu().numpy(), z["gin_x"], "x")
     assert all(p.grad is None for p in m.parameters())
+
+
+def test_input_grads_require_the_backward_of_the_latest_forward(cuda_device):
+    """cgr_gnn_input_grads reads dpre0 from the backward's workspace: without a backward of this
+    arena's forward, or with another workspace, it fails loudly instead of returning garbage
+    (ADVICE r05); with the backward's own workspace it runs."""
+    import ctypes
+
+    lib = native.load()
+    b = make_batch(4, n_atoms=12, n_bonds=13, n_mace=8, seed=3)
+    torch.manual_seed(0)
+    m = GNN(b.x.shape[1], 14, depth=2, hidden_sizes=[24] * 2, dropout_ps=[0.0] * 2)
+    m = m.to(cuda_device)
+    d = b.to_torch(cuda_device)
+    params = [p.detach() for p in m.native_parameters()]
+    run = ArenaRun(_cfg_tuple(b.x.shape[1], 14, 24, 2, "relu", False), d.x, d.edge_index,
+                   d.edge_attr, d.batch, d.ptr, b.num_graphs, params)
+    dy = torch.ones(b.num_graphs, device=cuda_device)
+    ws_other = torch.empty(lib.cgr_gnn_workspace_bytes(ctypes.byref(run.cfg), run.N, run.E,
+                                                       run.B), dtype=torch.uint8,
+                           device=cuda_device)
+    with pytest.raises(RuntimeError, match="workspace"):
+        run.input_grads(dy, params, ws_other)  # no backward yet
+    run.backward(dy, params)
+    with pytest.raises(RuntimeError, match="workspace"):
+        run.input_grads(dy, params, ws_other)  # not the backward's workspace
+    dx, de = run.input_grads(dy, params, run.ws)
+    torch.cuda.synchronize()
+    assert torch.isfinite(dx).all() and torch.isfinite(de).all()
 
 
 def test_cfg2_input_gradients_vs_oracle(cuda_device):
@@ -981,15 +1011,26 @@ def test_unpaired_timeout_raises_and_poisons(cuda_device, monkeypatch):
         m(data)  # first forward: the sync pairing check (warns), outside the timed-out backward
         monkeypatch.setenv("CGR_UNPAIRED_SPIN_LIMIT", "-1")
         torch.nn.MSELoss(reduction="sum")(m(data), data.y).backward()
+        # the fused Adam enqueued behind the poisoned backward (no host check in between, as
+        # in a replayed step) reads the error word on the device and leaves everything untouched
+        opt = FusedAdam(m.parameters(), lr=1e-3, amsgrad=True)
+        before = [p.detach().clone() for p in m.parameters()]
+        opt.step()
         torch.cuda.synchronize()
         monkeypatch.delenv("CGR_UNPAIRED_SPIN_LIMIT")
         assert torch.isnan(m.edge_init.weight.grad).any()
+        for p, q in zip(m.parameters(), before):
+            assert torch.equal(p.detach(), q)
+        assert all(float(opt.state[p]["step"]) == 0.0 for p in m.parameters())
         with pytest.raises(RuntimeError, match="timed out"):
             m(data)
         m.zero_grad(set_to_none=True)
         torch.nn.MSELoss(reduction="sum")(m(data), data.y).backward()
+        opt.step()  # the error was cleared by the raise: this step updates
         torch.cuda.synchronize()
     assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+    assert all(float(opt.state[p]["step"]) == 1.0 for p in m.parameters())
+    assert not all(torch.equal(p.detach(), q) for p, q in zip(m.parameters(), before))
     native.raise_device_errors(cuda_device)
 
 

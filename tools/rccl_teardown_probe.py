@@ -76,7 +76,7 @@ def main():
     gc.collect()
     torch.cuda.synchronize()
     say("all freed; ddp.teardown (hook closed, process group destroyed, then collected)")
-    teardown(m)
+    teardown(m, graphs_released=True)
     say("destroyed")
 
 
