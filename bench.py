@@ -397,6 +397,71 @@ def inference_measurement(model, data, B, dev, steps=50):
             "ms_per_batch": round(el / steps * 1e3, 4), "batch": B, "graph_captured": True}
 
 
+def single_reaction_measurement(model, cfgname, dev, calls=300, prof_calls=20):
+    """§8(f) rank 3, the reference's own inference call pattern: ONE reaction per forward, eval
+    mode, under no_grad -- test.py:85-113 (DataLoader batch_size 1: a one-graph Batch) and
+    cli_tool/activation_energy_predictor.py:72-76 (a single Data, batch=None).  Per pattern:
+    the median latency of `model(data)` + synchronize (the CLI reads each prediction), the host
+    time to enqueue one call (calls issued back to back), and the device time of one call's
+    kernels (library HIP events per kernel class, summed)."""
+    import numpy as np
+
+    from cgr_mpnn_3D._amd import native
+    from cgr_mpnn_3D._amd.synth import CONFIGS, TorchBatch, make_batch
+
+    c = CONFIGS[cfgname]
+    b = make_batch(1, c["n_atoms"], c["n_bonds"], c["n_mace"], seed=4242)
+    x = torch.from_numpy(b.x).to(dev)
+    ei = torch.from_numpy(b.edge_index).to(dev)
+    ea = torch.from_numpy(b.edge_attr).to(dev)
+    pats = {"batch_none_cli": TorchBatch(x, ei, ea, None),
+            "one_graph_batch_test_py": TorchBatch(x, ei, ea, torch.from_numpy(b.batch).to(dev),
+                                                  torch.from_numpy(b.ptr).to(dev))}
+    lib = native.load()
+    was = model.training
+    model.eval()
+    out = {"graph": f"one {cfgname}-shaped reaction: N={x.shape[0]} atoms, E={ei.shape[1]} "
+                    f"directed edges, F={x.shape[1]}"}
+    try:
+        with torch.no_grad():
+            for name, d in pats.items():
+                for _ in range(20):
+                    model(d)
+                torch.cuda.synchronize()
+                lat = []
+                for _ in range(calls):
+                    t0 = time.perf_counter()
+                    model(d)
+                    torch.cuda.synchronize()
+                    lat.append(time.perf_counter() - t0)
+                t0 = time.perf_counter()
+                for _ in range(100):
+                    model(d)
+                host = (time.perf_counter() - t0) / 100
+                torch.cuda.synchronize()
+                lib.cgr_profile_reset()
+                lib.cgr_profile_enable(1)
+                for _ in range(prof_calls):
+                    model(d)
+                torch.cuda.synchronize()
+                lib.cgr_profile_enable(0)
+                rep = native.profile_report()
+                dev_ms = sum(t for _, t in rep.values()) / prof_calls
+                launches = sum(n for n, _ in rep.values()) / prof_calls
+                out[name] = {"latency_us_median": round(float(np.median(lat)) * 1e6, 1),
+                             "latency_us_p90": round(float(np.percentile(lat, 90)) * 1e6, 1),
+                             "host_enqueue_us": round(host * 1e6, 1),
+                             "device_us": round(dev_ms * 1e3, 1),
+                             "kernel_classes_per_call": round(launches, 1),
+                             "device_us_by_class": {k: round(t / prof_calls * 1e3, 2)
+                                                    for k, (_, t) in sorted(rep.items())},
+                             "reactions_per_s": round(1.0 / float(np.median(lat)), 1)}
+    finally:
+        model.train(was)
+    out["single_reaction_us"] = out["batch_none_cli"]["latency_us_median"]
+    return out
+
+
 # ------------------------------------------------------------------------------------------------
 def host_cpu_info():
     """What the CPU baseline ran on: the CPU model, the machine's physical cores and logical
@@ -421,8 +486,15 @@ def host_cpu_info():
         allowed = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         allowed = None
+    quota = None  # cgroup v2 CPU bandwidth limit of this process ("max" = none), in CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return {"cpu_model": model, "machine_physical_cores": phys, "machine_logical_cpus": logical,
-            "process_allowed_cpus": allowed, "torch_threads": torch.get_num_threads(),
+            "process_allowed_cpus": allowed, "cgroup_cpu_quota": quota,
+            "torch_threads": torch.get_num_threads(),
             "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
@@ -434,7 +506,7 @@ def host_physical_cores():
     phys, logical = info["machine_physical_cores"], info["machine_logical_cpus"]
     if phys and logical:
         return max(1, round(allowed * phys / logical))
-    return allowed
+    return allowed  # (a cgroup CPU quota, if any, is recorded by host_cpu_info, not applied)
 
 
 def cpu_baseline_both(cfgname, seconds, dropout):
@@ -790,6 +862,18 @@ def main():
                                           traffic=hbm("segsum_dst_fwd"))
         roof_scatter["backward_gather_twin"] = dict(sc[("segsum_src_bwd", "cold")],
                                                     traffic=hbm("segsum_src_twin_cold"))
+        if args.config == "cfg2":
+            # the same kernel on cfg4's edge set (200-atom reactions, E = 204,800; 491 MB per
+            # launch, beyond the Infinity Cache with two rotating copies), same box, same run
+            from cgr_mpnn_3D._amd.synth import CONFIGS as _C, make_batch as _mb
+
+            c4 = _C["cfg4"]
+            b4 = _mb(c4["num_graphs"], c4["n_atoms"], c4["n_bonds"], 0, seed=1234)
+            sc4 = scatter_add_roofline(torch.from_numpy(b4.edge_index).to(dev), b4.x.shape[0], H,
+                                       dev, reps=20, cold_copies=2,
+                                       which=[("segsum_dst_fwd", "cold")])
+            roof_scatter["at_cfg4_edge_set"] = sc4[("segsum_dst_fwd", "cold")]
+            del b4, sc4
         # inside the step: the forward's scatter-adds run in the layer GEMM's epilogue (no
         # kernel of their own); the backward's Gs = segsum_src(dpre0) is a standalone one
         if "segsum_src_bwd" in rep:
@@ -805,6 +889,7 @@ def main():
     infer = None
     if rank == 0 and world == 1 and args.infer_bench:
         infer = inference_measurement(model, data, B, dev)
+        infer["single_reaction"] = single_reaction_measurement(model, args.config, dev)
         if args.profile_steps > 0:  # per-class device time of the forward-only path
             was = model.training
             model.eval()

@@ -86,16 +86,23 @@ def main():
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         step()
+    hrep = {}
+
+    def replay(name):
+        t = time.perf_counter()
+        g.replay()
+        hrep[name] = round((time.perf_counter() - t) * 1e6, 1)
+
     for i in range(args.warmup):
         stamp(f"warm{i}")
-        g.replay()
+        replay(f"warm{i}")
     torch.cuda.synchronize()
     if args.pre_spin_ms > 0:
         t0 = time.perf_counter()
         i = 0
         while time.perf_counter() - t0 < args.pre_spin_ms * 1e-3:
             stamp(f"spin{i}")
-            g.replay()
+            replay(f"spin{i}")
             i += 1
             if i % 20 == 0:
                 main_s.synchronize()
@@ -106,7 +113,7 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.steps):
             stamp(f"b{blk}s{i}")
-            g.replay()
+            replay(f"b{blk}s{i}")
         stamp(f"b{blk}end")
         torch.cuda.synchronize()
         host.append((time.perf_counter() - t0) / args.steps * 1e3)
@@ -120,7 +127,8 @@ def main():
     for i in range(len(names) - 1):
         steps.append({"name": names[i], "t_ms": round((st[i][0] - st[0][0]) * 1e-5, 4),
                       "dev_ms": round((st[i + 1][0] - st[i][2]) * 1e-5, 4),
-                      "clock_ghz": round(clk(st[i]), 3)})
+                      "clock_ghz": round(clk(st[i]), 3),
+                      "host_replay_us": hrep.get(names[i])})
     out = {"config": args.config, "steps": args.steps, "warmup": args.warmup,
            "pre_spin_ms": args.pre_spin_ms, "blocks": []}
     for blk in range(args.blocks + 1):
