@@ -161,3 +161,33 @@ def test_captured_batched_inference_replays(cuda_device):
         g.replay()
         torch.cuda.synchronize()
     assert torch.equal(out, ref)
+
+
+def test_single_reaction_calls_equal_the_batched_path(cuda_device):
+    """The reference's inference call pattern -- one reaction per model(data) under no_grad,
+    batch=None (cli_tool/activation_energy_predictor.py:72-76) or a one-graph Batch (test.py's
+    DataLoader batch_size 1, :85-113): both forms give the same prediction bit for bit, and the
+    batched forward of all reactions agrees within fp32 rounding (a dst segment that crosses a
+    row tile in the batch is summed as two partials)."""
+    from cgr_mpnn_3D._amd.synth import TorchBatch
+
+    b = make_batch(6, n_atoms=30, n_bonds=30, n_mace=768, seed=77, n_atoms_jitter=4)
+    m = _model(cuda_device, b.x.shape[1], 4, 400).eval()
+    data = b.to_torch(cuda_device)
+    with torch.no_grad():
+        y_batched = m(data)
+        singles = []
+        for g in range(b.num_graphs):
+            v0, v1 = int(b.ptr[g]), int(b.ptr[g + 1])
+            sel = torch.from_numpy((b.edge_index[0] >= v0) & (b.edge_index[0] < v1)).to(cuda_device)
+            x = data.x[v0:v1]
+            ei = (data.edge_index[:, sel] - v0).contiguous()
+            ea = data.edge_attr[sel].contiguous()
+            y_none = m(TorchBatch(x, ei, ea, None))
+            bt = torch.zeros(x.shape[0], dtype=torch.int64, device=cuda_device)
+            ptr = torch.tensor([0, x.shape[0]], dtype=torch.int64, device=cuda_device)
+            y_one = m(TorchBatch(x, ei, ea, bt, ptr))
+            assert y_none.shape == (1,) and torch.equal(y_none, y_one)
+            singles.append(y_none)
+    y_single = torch.cat(singles)
+    assert torch.allclose(y_single, y_batched, rtol=1e-5, atol=1e-6), (y_single, y_batched)
