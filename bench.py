@@ -723,7 +723,11 @@ def main():
         ok = 1
         try:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            # thread-local capture: the c10d / RCCL watchdog thread queries its own events while
+            # this thread captures, which a global-mode capture treats as an error (seen once on
+            # the RCCL world-1 rehearsal: "operation not permitted when stream is capturing")
+            with torch.cuda.graph(g, capture_error_mode="thread_local" if distributed
+                                  else "global"):
                 step()
         except Exception as exc:  # noqa: BLE001
             # a capture the runtime refuses (e.g. a collective RCCL cannot record at this world

@@ -70,7 +70,8 @@ def _captured(m, data):
             step()
     torch.cuda.current_stream().wait_stream(s)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    # thread-local: a live process group's watchdog thread queries events during the capture
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         out = step()
     g.replay()
     torch.cuda.synchronize()
