@@ -28,6 +28,21 @@ def test_library_loads_and_abi_version():
     assert lib.cgr_abi_version() == native.ABI_VERSION
 
 
+def test_library_was_built_from_these_sources():
+    """csrc/Makefile records the SHA-256 of every source beside the library it links
+    (cgr_mpnn_3D/_amd/buildinfo.py); a library stale against the tree fails here (and in
+    smoke()) instead of running silently (the .so ships prebuilt)."""
+    from cgr_mpnn_3D._amd import buildinfo
+
+    if os.path.abspath(native.LIB_PATH) != os.path.abspath(
+            os.path.join(os.path.dirname(buildinfo.INFO), os.path.basename(native.LIB_PATH))):
+        pytest.skip("CGR_MPNN3D_LIB points at another library")
+    info = buildinfo.check()
+    assert info.get("sources_sha256"), "no build record beside the library: rebuild (make)"
+    assert info["matches_sources"], "the library is stale against csrc/ and include/: rebuild"
+    assert "gfx950" in info["flags"]
+
+
 def test_every_declared_symbol_is_exported_and_bound():
     declared = _declared_functions()
     assert len(declared) >= 12
