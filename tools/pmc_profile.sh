@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-pmc}
 mkdir -p "$OUT"
 CFG=${CFG:-cfg2}
-ARGS="--config $CFG --steps ${STEPS:-3} --warmup 2 --cpu-baseline 0 --graph 0 --profile-steps 0"
+ARGS="--config $CFG --steps ${STEPS:-3} --warmup 2 --cpu-baseline 0 --graph 0 --profile-steps 0 --min-warmup-ms 0 --collate-bench 0 --infer-bench 0"
 run_pass() {
   local name=$1; shift
   echo "[pmc] $(date +%T) pass $name: $*"
