@@ -176,6 +176,11 @@ class GNNFunction(torch.autograd.Function):
         return (None, dx, None, dea) + (None,) * 8 + tuple(grads)
 
 
+# predict arena sizes by (config, N, E, B): a pure function of its key (one ctypes call saved per
+# call of the single-reaction loop)
+_PREDICT_ARENA_BYTES: dict = {}
+
+
 def gnn_predict(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, dropout_ps,
                 seed, training, params, rng_counter=None):
     """Forward-only GNN (cgr_gnn_predict): no saved activations.  What GNN.forward runs when no
@@ -187,9 +192,15 @@ def gnn_predict(cfg_tuple, x, edge_index, edge_attr, batch, graph_ptr, num_graph
     cfg = make_config(*cfg_tuple)
     N, E, B = int(x.shape[0]), int(edge_index.shape[1]), int(num_graphs)
     dev = x.device
-    nbytes = lib.cgr_gnn_predict_arena_bytes(ctypes.byref(cfg), N, E, B)
-    if nbytes < 0:
-        native.check(1)
+    key = (cfg_tuple, N, E, B)
+    nbytes = _PREDICT_ARENA_BYTES.get(key)
+    if nbytes is None:
+        nbytes = lib.cgr_gnn_predict_arena_bytes(ctypes.byref(cfg), N, E, B)
+        if nbytes < 0:
+            native.check(1)
+        if len(_PREDICT_ARENA_BYTES) > 4096:
+            _PREDICT_ARENA_BYTES.clear()
+        _PREDICT_ARENA_BYTES[key] = nbytes
     arena = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     y = torch.empty(B, dtype=torch.float32, device=dev)
     bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)

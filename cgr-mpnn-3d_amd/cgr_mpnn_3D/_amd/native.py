@@ -169,9 +169,15 @@ def stream_ptr(device) -> int:
 def device_guard(device):
     """Context making ``device`` the current HIP device around a native call: the C ABI enqueues
     on the stream it is given, but side streams, events and allocations follow the current
-    device, so a model on cuda:1 driven while cuda:0 is current must switch first."""
+    device, so a model on cuda:1 driven while cuda:0 is current must switch first.  A no-op
+    context when ``device`` is already current (the common case: no device switch per call)."""
+    import contextlib
+
     import torch
 
+    idx = device.index if isinstance(device, torch.device) else device
+    if idx is None or idx == torch.cuda.current_device():
+        return contextlib.nullcontext()
     return torch.cuda.device(device)
 
 

@@ -153,18 +153,25 @@ class GNN(nn.Module):
 
     # -- helpers -------------------------------------------------------------------------------
     def native_parameters(self):
-        """Parameters in the C-ABI table order (== reference state_dict order)."""
-        ps = [self.edge_init.weight, self.edge_init.bias]
-        for conv in self.convs:
-            ps += [conv.lin.weight, conv.lin.bias]
-        ps += [self.edge_to_node.weight, self.edge_to_node.bias, self.ffn.weight, self.ffn.bias]
+        """Parameters in the C-ABI table order (== reference state_dict order).  Read from the
+        submodules' parameter dicts directly (what nn.Module.__getattr__ resolves to, without its
+        per-access lookups: this runs on every forward, r06 single-reaction latency)."""
+        mods = self._modules
+        ei, en, ff = (mods["edge_init"]._parameters, mods["edge_to_node"]._parameters,
+                      mods["ffn"]._parameters)
+        ps = [ei["weight"], ei["bias"]]
+        for conv in mods["convs"]._modules.values():
+            lp = conv._modules["lin"]._parameters
+            ps += [lp["weight"], lp["bias"]]
+        ps += [en["weight"], en["bias"], ff["weight"], ff["bias"]]
         if self.use_learnable_skip:
-            ps += list(self.skip_weights)
+            ps += list(mods["skip_weights"]._parameters.values())
         return ps
 
     def _uniform_hidden(self) -> int:
-        widths = {self.edge_init.out_features, self.edge_to_node.out_features}
-        widths |= {conv.lin.out_features for conv in self.convs}
+        mods = self._modules
+        widths = {mods["edge_init"].out_features, mods["edge_to_node"].out_features}
+        widths |= {conv._modules["lin"].out_features for conv in mods["convs"]._modules.values()}
         if len(widths) != 1:
             raise RuntimeError(
                 f"GNN: hidden sizes {sorted(widths)} differ; the D-MPNN skip connection "
@@ -179,7 +186,7 @@ class GNN(nn.Module):
                 "cgr_mpnn_3D (MI355X) runs on the GPU only: move the model and the batch to "
                 "'cuda' (there is no CPU fallback)")
         pool = pooling_code(self.pooling_fn)
-        aggrs = {aggregation_code(conv.aggr) for conv in self.convs}
+        aggrs = {aggregation_code(conv.aggr) for conv in self._modules["convs"]._modules.values()}
         if len(aggrs) != 1:
             raise NotImplementedError("cgr_mpnn_3D (MI355X): one aggr for every DMPNNConv")
         aggr = aggrs.pop()
@@ -251,8 +258,9 @@ class GNN(nn.Module):
         if not (torch.is_grad_enabled() and want_grad):
             # no gradient wanted (test.py / the CLI run under torch.no_grad()): the forward-only
             # path, no saved activations
+            # (no autograd here: the raw parameters' data pointers, no detach)
             return gnn_predict(cfg, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, drop,
-                               seed, training, [p.detach() for p in params], rng_counter=counter)
+                               seed, training, params, rng_counter=counter)
         return gnn_forward(cfg, x, edge_index, edge_attr, batch, graph_ptr, num_graphs, drop,
                            seed, training, params, self._grad_bucket_hook, rng_counter=counter)
 
