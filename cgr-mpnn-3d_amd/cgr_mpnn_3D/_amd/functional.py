@@ -74,6 +74,49 @@ def grad_layout(shapes, depth):
     return offs, buckets, off
 
 
+_GRAD_VIEWS: dict = {}
+
+
+def _grad_views(params, depth):
+    """(per-parameter (shape, stride, offset) of its view into the flat gradient buffer, buckets,
+    total floats), memoised by the parameter shapes: grad_layout and the views' geometry are
+    pure functions of them (the host cost of the eager backward, r06)."""
+    key = (depth,) + tuple(p.shape for p in params)
+    hit = _GRAD_VIEWS.get(key)
+    if hit is None:
+        offs, buckets, total = grad_layout(key[1:], depth)
+        geo = []
+        for o, p in zip(offs, params):
+            shape = tuple(p.shape)
+            stride, acc = [], 1
+            for d in reversed(shape):
+                stride.append(acc)
+                acc *= int(d)
+            geo.append((shape, tuple(reversed(stride)), o))
+        if len(_GRAD_VIEWS) > 64:
+            _GRAD_VIEWS.clear()
+        hit = _GRAD_VIEWS[key] = (tuple(geo), buckets, total)
+    return hit
+
+
+# training arena / workspace sizes by (config, N, E, B): pure functions of their key
+_ARENA_BYTES: dict = {}
+_WS_BYTES: dict = {}
+
+
+def _memo_bytes(memo, fn, cfg, cfg_tuple, N, E, B):
+    key = (cfg_tuple, N, E, B)
+    n = memo.get(key)
+    if n is None:
+        n = fn(ctypes.byref(cfg), N, E, B)
+        if n < 0:
+            native.check(1)
+        if len(memo) > 4096:
+            memo.clear()
+        memo[key] = n
+    return n
+
+
 def read_status(arena, cfg, N, E, B) -> int:
     """Graph-prep status word (bit0 bad edge index, bit1 bad/unsorted batch, bit2 edges not
     reverse-paired: informational, bit4 the unpaired backward's completion timed out).
@@ -93,9 +136,7 @@ class GNNFunction(torch.autograd.Function):
         cfg = make_config(*cfg_tuple)
         N, E, B = int(x.shape[0]), int(edge_index.shape[1]), int(num_graphs)
         dev = x.device
-        arena_bytes = lib.cgr_gnn_arena_bytes(ctypes.byref(cfg), N, E, B)
-        if arena_bytes < 0:
-            native.check(1)
+        arena_bytes = _memo_bytes(_ARENA_BYTES, lib.cgr_gnn_arena_bytes, cfg, cfg_tuple, N, E, B)
         arena = torch.empty(arena_bytes, dtype=torch.uint8, device=dev)
         y = torch.empty(B, dtype=torch.float32, device=dev)
         bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
@@ -133,12 +174,12 @@ class GNNFunction(torch.autograd.Function):
         cfg = make_config(*ctx.cfg_tuple)
         N, E, B = int(x.shape[0]), int(edge_index.shape[1]), ctx.num_graphs
         dev = x.device
-        ws = torch.empty(lib.cgr_gnn_workspace_bytes(ctypes.byref(cfg), N, E, B),
-                         dtype=torch.uint8, device=dev)
+        ws = torch.empty(_memo_bytes(_WS_BYTES, lib.cgr_gnn_workspace_bytes, cfg, ctx.cfg_tuple,
+                                     N, E, B), dtype=torch.uint8, device=dev)
         # one flat gradient buffer in all-reduce bucket order, viewed per parameter
-        offs, buckets, total = grad_layout([tuple(p.shape) for p in params], cfg.depth)
+        geo, buckets, total = _grad_views(params, cfg.depth)
         flat = torch.empty(total, dtype=torch.float32, device=dev)
-        grads = [flat[o:o + p.numel()].view(p.shape) for o, p in zip(offs, params)]
+        grads = [flat.as_strided(s, st, o) for s, st, o in geo]
         dy = dy.contiguous().float()
         bs = _batch_struct(x, edge_index, edge_attr, batch, graph_ptr, B)
         hook = ctx.bucket_hook if ctx.bucket_hook is not None else _config.grad_bucket_hook

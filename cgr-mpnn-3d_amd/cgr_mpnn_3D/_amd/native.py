@@ -160,10 +160,24 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
+_raw_stream = None
+
+
 def stream_ptr(device) -> int:
+    """hipStream_t of ``device``'s current stream.  Read through torch's raw-stream accessor
+    (the pointer alone, no Stream object: ~0.3 us instead of ~4 us, three times per training
+    step); torch.cuda.current_stream() where that accessor is absent."""
+    global _raw_stream
     import torch
 
-    return torch.cuda.current_stream(device).cuda_stream
+    if _raw_stream is None:
+        _raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", False)
+    idx = getattr(device, "index", device)
+    if idx is None:
+        idx = torch.cuda.current_device()
+    if _raw_stream:
+        return _raw_stream(idx)
+    return torch.cuda.current_stream(idx).cuda_stream
 
 
 def device_guard(device):

@@ -15,6 +15,7 @@ Parameters must be fp32 CUDA tensors; there is no CPU fallback.
 from __future__ import annotations
 
 import ctypes
+import operator
 
 import torch
 
@@ -59,31 +60,75 @@ class FusedAdam(torch.optim.Optimizer):
                     st[k] = v.to(device=p.device, dtype=torch.float32).contiguous()
         return st
 
+    _STATE_KEYS = ("exp_avg", "exp_avg_sq", "max_exp_avg_sq", "step")
+
+    def _table(self, gi, params, grads):
+        """The group's CgrAdamTensor table.  Built once and kept while the group's parameters,
+        their state tensors and the state dict itself are the same objects (load_state_dict
+        replaces the dict, so it rebuilds); per step only the parameter and gradient pointers are
+        rewritten.  Every gradient is still checked (fp32, contiguous) each step."""
+        for g in grads:
+            if g.dtype != torch.float32 or not g.is_contiguous():
+                raise RuntimeError("FusedAdam: contiguous float32 params/grads required")
+        cache = self.__dict__.setdefault("_cgr_tables", {})
+        hit = cache.get(gi)
+        if hit is not None:
+            state, ps, sts, tab = hit
+            ok = state is self.state and len(ps) == len(params)
+            if ok:
+                for p, q, s in zip(params, ps, sts):
+                    st = state.get(p)
+                    if p is not q or st is None or \
+                            not all(map(operator.is_, map(st.get, self._STATE_KEYS), s)):
+                        ok = False
+                        break
+            if ok:
+                for i, (p, g) in enumerate(zip(params, grads)):
+                    e = tab[i]
+                    if e.numel != p.numel():  # p.data was replaced by a tensor of another size
+                        ok = False
+                        break
+                    e.param, e.grad = p.data_ptr(), g.data_ptr()
+            if ok:
+                return tab
+        sts = []
+        tab = (native.CgrAdamTensor * len(params))()
+        for i, (p, g) in enumerate(zip(params, grads)):
+            st = self._init_state(p)
+            if not p.is_contiguous():
+                raise RuntimeError("FusedAdam: contiguous float32 params/grads required")
+            s = tuple(st[k] for k in self._STATE_KEYS)
+            sts.append(s)
+            tab[i] = native.CgrAdamTensor(p.data_ptr(), g.data_ptr(), s[0].data_ptr(),
+                                          s[1].data_ptr(), s[2].data_ptr(), s[3].data_ptr(),
+                                          p.numel())
+        dev = params[0].device
+        if any(p.device != dev for p in params):
+            raise RuntimeError("FusedAdam: all parameters of a group must be on one device")
+        cache[gi] = (self.state, list(params), sts, tab)
+        return tab
+
+    def __setstate__(self, state):
+        super().__setstate__(state)
+        self.__dict__.pop("_cgr_tables", None)
+
     @torch.no_grad()
     def step(self, closure=None):
         loss = None
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        for group in self.param_groups:
-            ps = [p for p in group["params"] if p.grad is not None]
+        for gi, group in enumerate(self.param_groups):
+            ps = group["params"]
+            grads = [p.grad for p in ps]
+            if any(g is None for g in grads):
+                ps = [p for p, g in zip(ps, grads) if g is not None]
+                grads = [g for g in grads if g is not None]
             if not ps:
                 continue
             beta1, beta2 = group["betas"]
-            tab = (native.CgrAdamTensor * len(ps))()
-            for i, p in enumerate(ps):
-                st = self._init_state(p)
-                g = p.grad
-                if g.dtype != torch.float32 or not g.is_contiguous() or not p.is_contiguous():
-                    raise RuntimeError("FusedAdam: contiguous float32 params/grads required")
-                tab[i] = native.CgrAdamTensor(p.data_ptr(), g.data_ptr(),
-                                              st["exp_avg"].data_ptr(),
-                                              st["exp_avg_sq"].data_ptr(),
-                                              st["max_exp_avg_sq"].data_ptr(),
-                                              st["step"].data_ptr(), p.numel())
+            tab = self._table(gi, ps, grads)
             dev = ps[0].device
-            if any(p.device != dev for p in ps):
-                raise RuntimeError("FusedAdam: all parameters of a group must be on one device")
             with native.device_guard(dev):
                 native.check(self._lib.cgr_adam_step(
                     tab, len(ps), float(group["lr"]), float(beta1), float(beta2),

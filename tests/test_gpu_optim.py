@@ -75,6 +75,52 @@ def test_fused_adam_loads_torch_adam_state(cuda_device):
         torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)
 
 
+def test_fused_adam_table_follows_state_and_parameter_changes(cuda_device):
+    """The per-group pointer table is reused across steps (r06 host trim): a reloaded state dict,
+    a replaced state tensor, `p.data` moved to new storage and a group that gains a gradient must
+    all reach the kernel (checked against torch.optim.Adam after each change)."""
+    ps_ref = _tensors(cuda_device, [(40, 9), (9,), (5, 5), ()], 5)
+    ps = [p.detach().clone().requires_grad_() for p in ps_ref]
+    ref = torch.optim.Adam(ps_ref, lr=2e-2, amsgrad=True)
+    opt = FusedAdam(ps, lr=2e-2, amsgrad=True)
+    g = torch.Generator().manual_seed(9)
+
+    def both_step(skip=None):
+        for i, (p, q) in enumerate(zip(ps, ps_ref)):
+            gr = torch.randn(p.shape, generator=g).to(cuda_device)
+            p.grad = None if i == skip else gr.clone()
+            q.grad = None if i == skip else gr.clone()
+        opt.step()
+        ref.step()
+
+    def same():
+        torch.cuda.synchronize()
+        for a, b in zip(ps, ps_ref):
+            torch.testing.assert_close(a.detach(), b.detach(), rtol=1e-5, atol=1e-6)
+            sa, sb = opt.state[a], ref.state[b]
+            for k in ("exp_avg", "exp_avg_sq", "max_exp_avg_sq"):
+                torch.testing.assert_close(sa[k], sb[k], rtol=1e-5, atol=1e-6)
+
+    both_step()
+    both_step()
+    same()
+    opt.load_state_dict(copy.deepcopy(opt.state_dict()))  # a new state dict
+    both_step()
+    same()
+    st = opt.state[ps[0]]
+    st["exp_avg"] = st["exp_avg"].clone()  # a replaced state tensor
+    both_step()
+    same()
+    for p, q in zip(ps, ps_ref):  # new storage under the same parameter objects
+        p.data = p.data.clone()
+        q.data = q.data.clone()
+    both_step()
+    same()
+    both_step(skip=1)  # one parameter without a gradient this step, then back
+    both_step()
+    same()
+
+
 def test_fused_adam_many_tensors_and_misaligned_grads(cuda_device):
     # > CGR_ADAM_GROUP tensors (several launches) and grads that are views at odd offsets of one
     # flat buffer (the native backward's bucket layout): scalar path for those tensors
