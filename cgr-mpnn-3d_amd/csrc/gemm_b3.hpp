@@ -259,6 +259,10 @@ struct B3NtShape {
 #endif
 constexpr int B3_LDA = CGR_B3_LDA;  // B fragment groups read from LDS ahead of the MFMAs using them
 constexpr bool kB3ReadAheadFence = CGR_B3_RA_FENCE;
+#ifndef CGR_B3_STEP_ACC
+#define CGR_B3_STEP_ACC 0
+#endif
+constexpr bool kB3StepAcc = CGR_B3_STEP_ACC;
 
 // Pipeline (one barrier per k step, 3 LDS buffers for B):
 //   iteration ks computes step ks from LDS buffer ks % 3 and A fragments afr[ks & 1], and stages
@@ -425,6 +429,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     // the read-ahead is issued here, ahead of everything (else the scheduler fills each pair's
     // ds_read group with that pair's own reads and waits on them right away)
     if constexpr (kB3ReadAheadFence) __builtin_amdgcn_sched_barrier(0);
+    floatx4 carx[RF], cary[RF];  // kB3StepAcc: the previous pair's step sums
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int j = 2 * p;
@@ -442,7 +447,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       const b3_u4(&c)[3] = bq[(j + 1) % RING];
 #pragma unroll
       for (int i = 0; i < RF; ++i) {
-        floatx4 x = acc[i][j], y = two ? acc[i][j + 1] : x;
+        // kB3StepAcc: the step's six products into a zero accumulator, then one fp32 add into
+        // the running sum (the matrix core aligns every product of an MFMA to its largest
+        // operand, accumulator included: the small pieces' products would be rounded at the
+        // running sum's ulp, tools/diag/bf16_round_probe.hip).  The add of pair p is issued
+        // behind pair p + 1's MFMAs (carry): only two pairs' temporaries are live.
+        floatx4 x = kB3StepAcc ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i][j];
+        floatx4 y = kB3StepAcc ? x : (two ? acc[i][j + 1] : x);
         x = b3_mfma(afc[i][1], b[1], x);
         if (two) y = b3_mfma(afc[i][1], c[1], y);
         x = b3_mfma(afc[i][0], b[2], x);
@@ -455,8 +466,17 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         if (two) y = b3_mfma(afc[i][1], c[0], y);
         x = b3_mfma(afc[i][0], b[0], x);
         if (two) y = b3_mfma(afc[i][0], c[0], y);
-        acc[i][j] = x;
-        if (two) acc[i][j + 1] = y;
+        if constexpr (kB3StepAcc) {
+          if (p > 0) {
+            acc[i][j - 2] += carx[i];
+            acc[i][j - 1] += cary[i];  // the previous pair always has two columns
+          }
+          carx[i] = x;
+          cary[i] = y;
+        } else {
+          acc[i][j] = x;
+          if (two) acc[i][j + 1] = y;
+        }
       }
       // this pair's share of the load slots and of the B stores
       int nvm = 0, nst = 0;
@@ -484,6 +504,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       if (two) b3_sgb<0x008>(MQ); else b3_sgb<0x008>(MQ / 2);
       b3_sgb<0x200>(nst);                                    // ds_write
       if (two) b3_sgb<0x008>(MQ); else b3_sgb<0x008>(MQ);
+    }
+    if constexpr (kB3StepAcc) {  // the last pair's step sums
+      constexpr int jl = 2 * (NP - 1);
+#pragma unroll
+      for (int i = 0; i < RF; ++i) {
+        acc[i][jl] += carx[i];
+        if constexpr (jl + 1 < NF) acc[i][jl + 1] += cary[i];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
@@ -525,6 +553,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
 #pragma unroll
     for (int j = 0; j < LDA; ++j) rd(j);
     if constexpr (kB3ReadAheadFence) __builtin_amdgcn_sched_barrier(0);
+    floatx4 carx[RF], cary[RF];  // kB3StepAcc: the previous pair's step sums
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int j = 2 * p;
@@ -542,7 +571,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       const b3_u4(&c)[3] = bq[(j + 1) % RING];
 #pragma unroll
       for (int i = 0; i < RF; ++i) {
-        floatx4 x = acc[i][j], y = two ? acc[i][j + 1] : x;
+        // kB3StepAcc: the step's six products into a zero accumulator, then one fp32 add into
+        // the running sum (the matrix core aligns every product of an MFMA to its largest
+        // operand, accumulator included: the small pieces' products would be rounded at the
+        // running sum's ulp, tools/diag/bf16_round_probe.hip).  The add of pair p is issued
+        // behind pair p + 1's MFMAs (carry): only two pairs' temporaries are live.
+        floatx4 x = kB3StepAcc ? floatx4{0.f, 0.f, 0.f, 0.f} : acc[i][j];
+        floatx4 y = kB3StepAcc ? x : (two ? acc[i][j + 1] : x);
         x = b3_mfma(afc[i][1], b[1], x);
         if (two) y = b3_mfma(afc[i][1], c[1], y);
         x = b3_mfma(afc[i][0], b[2], x);
@@ -555,8 +590,17 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         if (two) y = b3_mfma(afc[i][1], c[0], y);
         x = b3_mfma(afc[i][0], b[0], x);
         if (two) y = b3_mfma(afc[i][0], c[0], y);
-        acc[i][j] = x;
-        if (two) acc[i][j + 1] = y;
+        if constexpr (kB3StepAcc) {
+          if (p > 0) {
+            acc[i][j - 2] += carx[i];
+            acc[i][j - 1] += cary[i];  // the previous pair always has two columns
+          }
+          carx[i] = x;
+          cary[i] = y;
+        } else {
+          acc[i][j] = x;
+          if (two) acc[i][j + 1] = y;
+        }
       }
       int nvm = 0;
       if (ADD && prefetch) {
@@ -570,6 +614,14 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
       if (two) b3_sgb<0x008>(MQ); else b3_sgb<0x008>(MQ / 2);
       b3_sgb<0x020>(nvm);
       if (two) b3_sgb<0x008>(2 * MQ); else b3_sgb<0x008>(MQ + MQ / 2);
+    }
+    if constexpr (kB3StepAcc) {  // the last pair's step sums
+      constexpr int jl = 2 * (NP - 1);
+#pragma unroll
+      for (int i = 0; i < RF; ++i) {
+        acc[i][jl] += carx[i];
+        if constexpr (jl + 1 < NF) acc[i][jl + 1] += cary[i];
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (last) __syncthreads();
