@@ -95,16 +95,17 @@ struct EpLayerBwdSeg {
 
   // C: the tile's accumulators [BM][LDC] in LDS (column j of the tile = output column n0 + j);
   // sd[q]: dst of rows m0 - 1 + q (q < BM + 2; distinct negative sentinels outside [0, M)),
-  // followed by 16 words of scratch; thread tid < RPP * C4 owns the float4 column group
-  // tid % C4 of rows tid / C4 + RPP * it, and pv[it] holds pre4 of those pieces;
+  // followed by 16 words of scratch; RPP > 0: thread tid < RPP * C4 owns the float4 column group
+  // tid % C4 of rows tid / C4 + RPP * it; RPP == 0 (flat): pass it takes piece q = tid + NT * it
+  // of the tile's BM x C4, row q / C4, column group q % C4; pv[it] holds pre4 of pass it's piece;
   // tile_id: this workgroup's tile (tm * tiles_n + tn)
   template <int BM, int BN, int NT, int LDC, int EIT, int RPP>
   __device__ __forceinline__ void tile(const Pre (&pv)[EIT], float* C, const int* sd, int m0,
                                        int n0, int tile_id, int tid) const {
     constexpr int C4 = BN / 4;
-    const bool eact = tid < RPP * C4;
-    const int ec4 = eact ? tid % C4 : 0, er0 = tid / C4;
-    const int col = n0 + 4 * ec4;
+    constexpr bool FLAT = RPP == 0;
+    const bool eact = FLAT || tid < RPP * C4;
+    const int ec4 = FLAT ? 0 : (eact ? tid % C4 : 0), er0 = FLAT ? 0 : tid / C4;
     const int nrow = min(BM, M - m0);
     const bool paired = (*status & 4) == 0;
     int* scratch = const_cast<int*>(sd) + BM + 2;  // 16 words
@@ -126,9 +127,19 @@ struct EpLayerBwdSeg {
       constexpr int A = decltype(Ac)::value;
 #pragma unroll
       for (int it = 0; it < EIT; ++it) {
-        const int r = er0 + RPP * it;
+        int r, c4;
+        if constexpr (FLAT) {
+          const int q = tid + NT * it;
+          if (q >= BM * C4) break;
+          r = q / C4;
+          c4 = q - r * C4;
+        } else {
+          r = er0 + RPP * it;
+          c4 = ec4;
+        }
+        const int col = n0 + 4 * c4;
         if (!eact || r >= nrow || col >= N) continue;
-        const float4 x = *reinterpret_cast<const float4*>(&C[r * LDC + 4 * ec4]);
+        const float4 x = *reinterpret_cast<const float4*>(&C[r * LDC + 4 * c4]);
         const int64_t i = m0 + r;
         if (!paired) {
           sc1_store4(raw + i * a.Hp + col, x);
@@ -139,7 +150,7 @@ struct EpLayerBwdSeg {
         const bool head = s == 0 && sd[0] == v, tail = e == nrow && sd[nrow + 1] == v;
         float4 da = f4zero();
         for (int k = s; k < e; ++k)
-          da = f4add(da, *reinterpret_cast<const float4*>(&C[k * LDC + 4 * ec4]));
+          da = f4add(da, *reinterpret_cast<const float4*>(&C[k * LDC + 4 * c4]));
         if (head || tail) {
           sc1_store4(raw + i * a.Hp + col, x);
           if (r == s) {
@@ -152,7 +163,7 @@ struct EpLayerBwdSeg {
               atomicAdd(g + 3, da.w);
             } else {
               const int slot = slot_of(m0 / BM, b / BM);
-              sc1_store4(part + ((int64_t)tile_id * 2 + slot) * BN + 4 * ec4, da);
+              sc1_store4(part + ((int64_t)tile_id * 2 + slot) * BN + 4 * c4, da);
             }
           }
         } else {

@@ -232,7 +232,7 @@ struct b3_ep_side<EP, std::void_t<decltype(EP::kSideBlock)>> : std::bool_constan
 // dynamic LDS bytes of a BM x BN NT workgroup (B3NtShape::LDS_BYTES)
 constexpr size_t b3nt_lds_bytes(int BM, int BN) {
   const size_t stage = (size_t)3 * (3 * BN * 4) * 16;
-  const size_t epi = (size_t)BM * (BN + 4) * 4 + (size_t)(BM + 2) * 4 + 64;
+  const size_t epi = (size_t)BM * (BN + 4) * 4 + (size_t)(BM + 2) * 4 + 64 + (size_t)(BM + 1) * 4;
   return stage > epi ? stage : epi;
 }
 
@@ -244,9 +244,10 @@ struct B3NtShape {
   static constexpr int BPT = (BU4 + NT - 1) / NT;
   static constexpr int LDC = BN + 4;
   static constexpr size_t STAGE_BYTES = 3 * BU4 * 16;
-  // + the dst of rows m0 - 1 .. m0 + BM (EpLayerSeg, EpLayerBwdSeg) and 16 floats of reduction
+  // + the dst of rows m0 - 1 .. m0 + BM (EpLayerSeg, EpLayerBwdSeg), 16 floats of reduction
   // scratch (EpLayerBwdSeg; kernels with static LDS cannot be given the full 160 KB dynamically)
-  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4 + 64;
+  // and the tile's segment-start rows + terminator (EpLayerSeg's segment pass)
+  static constexpr size_t EPI_BYTES = (size_t)BM * LDC * 4 + (BM + 2) * 4 + 64 + (BM + 1) * 4;
   static constexpr size_t LDS_BYTES = STAGE_BYTES > EPI_BYTES ? STAGE_BYTES : EPI_BYTES;
   static_assert(LDS_BYTES == b3nt_lds_bytes(BM, BN), "b3nt_lds_bytes");
 };
@@ -263,6 +264,10 @@ constexpr bool kB3ReadAheadFence = CGR_B3_RA_FENCE;
 #define CGR_B3_STEP_ACC 0
 #endif
 constexpr bool kB3StepAcc = CGR_B3_STEP_ACC;
+#ifndef CGR_B3_FLAT
+#define CGR_B3_FLAT 1
+#endif
+constexpr bool kB3FlatEpilogue = CGR_B3_FLAT;  // flat epilogue passes + compact segment pass
 
 // Pipeline (one barrier per k step, 3 LDS buffers for B):
 //   iteration ks computes step ks from LDS buffer ks % 3 and A fragments afr[ks & 1], and stages
@@ -311,6 +316,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   const bool eact = tid < RPP * C4;
   const int ec4 = eact ? tid % C4 : 0, er0 = tid / C4;
   const int ecol = n0 + 4 * ec4;
+  // Flat passes: epilogues without per-column constants (the addend forms, whose column terms
+  // are already in the accumulators; the whole-tile functors) take item q = tid + NT * it of the
+  // tile's BM x C4 float4 pieces, row q / C4, column group q % C4 -- every lane busy in every
+  // pass (at BM 128 x 52 groups: 13 passes of 512 instead of 15 passes of 468 lanes)
+  constexpr bool FLAT = kB3FlatEpilogue && (TILE || b3_ep_addend<EP>::value);
+  constexpr int EITF = (BM * C4 + NT - 1) / NT;
+  constexpr int EP_IT = FLAT ? EITF : EIT;
   // issued in the prologue behind the first operand loads, used after the main loop: the column
   // group's constants (bias, ...) and, for the segmented epilogues, the dst of rows
   // m0 - 1 .. m0 + BM (one per thread)
@@ -679,10 +691,18 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         for (int r = 0; r < 4; ++r)
           acc[i][j][r] = ep.add_apply(acc[i][j][r], arow_v[i][j][r], acol_v[j], cx);
   }
-  typename EP::Pre pv[EIT];
+  typename EP::Pre pv[EP_IT];
   if constexpr (!ADD) {
 #pragma unroll
-    for (int it = 0; it < EIT; ++it) pv[it] = ep.pre4(m0 + min(er0 + RPP * it, BM - 1), ecol);
+    for (int it = 0; it < EP_IT; ++it) {
+      if constexpr (FLAT) {
+        const int q = min(tid + NT * it, BM * C4 - 1);
+        const int r = q / C4;
+        pv[it] = ep.pre4(m0 + r, n0 + 4 * (q - r * C4));
+      } else {
+        pv[it] = ep.pre4(m0 + min(er0 + RPP * it, BM - 1), ecol);
+      }
+    }
   }
   float* C = reinterpret_cast<float*>(b3_lds);
   int* sd = reinterpret_cast<int*>(C + BM * S::LDC);  // SEG / TILE: dst of rows m0 - 1 .. m0 + BM
@@ -710,25 +730,59 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   __syncthreads();
   CGR_STAMP(3);
   if constexpr (TILE) {
-    ep.template tile<BM, BN, NT, S::LDC, EIT, RPP>(pv, C, sd, m0, n0, tile, tid);
+    ep.template tile<BM, BN, NT, S::LDC, EP_IT, FLAT ? 0 : RPP>(pv, C, sd, m0, n0, tile, tid);
   } else {
+  // SEG: the tile's segment-start rows in order, then the row count (the segment pass's items);
+  // written here, read behind the barrier that ends the apply pass
+  int* slist = sd + BM + 2 + 16;
+  const int nrow_t = min(BM, M - m0);
+  uint64_t mlo = 0, mhi = 0;
+  int nseg = 0;
+  if constexpr (SEG && FLAT) {
+    mlo = smask[0] | ((uint64_t)smask[1] << 32);
+    mhi = smask[2] | ((uint64_t)smask[3] << 32);
+    // starts among rows < nrow_t (rows past the tile's count are sentinel starts)
+    const uint64_t klo = nrow_t >= 64 ? mlo : mlo & ((1ull << nrow_t) - 1);
+    const uint64_t khi = nrow_t >= 128 ? mhi : (nrow_t > 64 ? mhi & ((1ull << (nrow_t - 64)) - 1) : 0);
+    nseg = __popcll(klo) + __popcll(khi);
+    if (tid < nrow_t && seg_bit(mlo, mhi, tid)) {
+      const int below = tid < 64 ? __popcll(mlo & ((1ull << tid) - 1))
+                                 : __popcll(mlo) + __popcll(mhi & ((1ull << (tid - 64)) - 1));
+      slist[below] = tid;
+    }
+    if (tid == 0) slist[nseg] = nrow_t;
+  }
   auto apply_pass = [&](auto Ac) {
     constexpr int A = decltype(Ac)::value;
+    if constexpr (FLAT) {
 #pragma unroll
-    for (int it = 0; it < EIT; ++it) {
-      const int r = er0 + RPP * it;
-      if (eact && r < BM) {
-        float4* cp = reinterpret_cast<float4*>(&C[r * S::LDC + 4 * ec4]);
-        if constexpr (SEG && ADD)
-          *cp = ep.template apply4z_h<A>(m0 + r, ecol, *cp, cx);  // keep h for the sums
-        else if constexpr (SEG)
-          *cp = ep.template apply4p_h<A>(m0 + r, ecol, *cp, pv[it], cx);
-        else if constexpr (ADD)
-          ep.template apply4z<A>(m0 + r, ecol, *cp, cx);
-        else if constexpr (b3_ep_act<EP>::value)
-          ep.template apply4p<A>(m0 + r, ecol, *cp, pv[it], cx);
+      for (int it = 0; it < EP_IT; ++it) {
+        const int q = tid + NT * it;
+        if (q >= BM * C4) break;
+        const int r = q / C4, c4 = q - r * C4, col = n0 + 4 * c4;
+        float4* cp = reinterpret_cast<float4*>(&C[r * S::LDC + 4 * c4]);
+        if constexpr (SEG)
+          *cp = ep.template apply4z_h<A>(m0 + r, col, *cp, cx);  // keep h for the sums
         else
-          ep.apply4p(m0 + r, ecol, *cp, pv[it], cx);
+          ep.template apply4z<A>(m0 + r, col, *cp, cx);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < EIT; ++it) {
+        const int r = er0 + RPP * it;
+        if (eact && r < BM) {
+          float4* cp = reinterpret_cast<float4*>(&C[r * S::LDC + 4 * ec4]);
+          if constexpr (SEG && ADD)
+            *cp = ep.template apply4z_h<A>(m0 + r, ecol, *cp, cx);  // keep h for the sums
+          else if constexpr (SEG)
+            *cp = ep.template apply4p_h<A>(m0 + r, ecol, *cp, pv[it], cx);
+          else if constexpr (ADD)
+            ep.template apply4z<A>(m0 + r, ecol, *cp, cx);
+          else if constexpr (b3_ep_act<EP>::value)
+            ep.template apply4p<A>(m0 + r, ecol, *cp, pv[it], cx);
+          else
+            ep.apply4p(m0 + r, ecol, *cp, pv[it], cx);
+        }
       }
     }
   };
@@ -749,22 +803,22 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     // node, in-degree > BM + 1) leaves its partial in a slot fixed by the data and its last
     // contributor sums the slots in row-tile order -- deterministic for every in-degree.
     __syncthreads();
-    const int nrow = min(BM, M - m0);
-    const uint64_t mlo = smask[0] | ((uint64_t)smask[1] << 32);
-    const uint64_t mhi = smask[2] | ((uint64_t)smask[3] << 32);
-#pragma unroll
-    for (int it = 0; it < EIT; ++it) {
-      const int r = er0 + RPP * it;
-      if (!eact || r >= nrow || ecol >= ep.N || !seg_bit(mlo, mhi, r)) continue;
-      const int e = seg_end(mlo, mhi, r);
+    const int nrow = nrow_t;
+    if constexpr (!FLAT) {
+      mlo = smask[0] | ((uint64_t)smask[1] << 32);
+      mhi = smask[2] | ((uint64_t)smask[3] << 32);
+    }
+    // segment [r, e) x column group c4
+    auto seg_item = [&](int r, int e, int c4) {
+      const int col = n0 + 4 * c4;
       const int v = sd[r + 1];
       float4 a = f4zero();
       for (int k = r; k < e; ++k)
-        a = f4add(a, *reinterpret_cast<const float4*>(&C[k * S::LDC + 4 * ec4]));
-      float* dst = ep.aout + (int64_t)v * ep.lda + ecol;
+        a = f4add(a, *reinterpret_cast<const float4*>(&C[k * S::LDC + 4 * c4]));
+      float* dst = ep.aout + (int64_t)v * ep.lda + col;
       const bool head = r == 0 && sd[0] == v, tail = e == nrow && sd[nrow + 1] == v;
       if (tail && !head && ep.znext)  // the tile where a crossing segment starts
-        *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + ecol) = f4zero();
+        *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + col) = f4zero();
       if (head || tail) {
         const int b = ep.dst_ptr[v], ee = ep.dst_ptr[v + 1];
         if (seg_tiles(b, ee, BM) <= 2) {
@@ -773,10 +827,29 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
           atomicAdd(dst + 2, a.z);
           atomicAdd(dst + 3, a.w);
         } else {
-          sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * ec4, a);
+          sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * c4, a);
         }
       } else {
         st4_nt(dst, a);  // (common.hpp)
+      }
+    };
+    if constexpr (FLAT) {
+      // items (segment j, column group c4) of the compact segment list: no lane waits on a
+      // row that does not start a segment
+#pragma unroll
+      for (int it = 0; it < EITF; ++it) {
+        const int q = tid + NT * it;
+        if (q >= nseg * C4) break;
+        const int j = q / C4, c4 = q - j * C4;
+        if (n0 + 4 * c4 >= ep.N) continue;
+        seg_item(slist[j], slist[j + 1], c4);
+      }
+    } else {
+#pragma unroll
+      for (int it = 0; it < EIT; ++it) {
+        const int r = er0 + RPP * it;
+        if (!eact || r >= nrow || ecol >= ep.N || !seg_bit(mlo, mhi, r)) continue;
+        seg_item(r, seg_end(mlo, mhi, r), ec4);
       }
     }
     // hub segments: the last contributor sums the slots of every row tile in order
