@@ -268,6 +268,10 @@ constexpr bool kB3StepAcc = CGR_B3_STEP_ACC;
 #define CGR_B3_FLAT 1
 #endif
 constexpr bool kB3FlatEpilogue = CGR_B3_FLAT;  // flat epilogue passes + compact segment pass
+#ifndef CGR_B3_SEGMERGE
+#define CGR_B3_SEGMERGE 1
+#endif
+constexpr bool kB3SegMerge = CGR_B3_SEGMERGE;  // the forward's apply and segment sums in one pass
 
 // Pipeline (one barrier per k step, 3 LDS buffers for B):
 //   iteration ks computes step ks from LDS buffer ks % 3 and A fragments afr[ks & 1], and stages
@@ -717,6 +721,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         smask[2 * (tid >> 6)] = (uint32_t)b;
         smask[2 * (tid >> 6) + 1] = (uint32_t)(b >> 32);
       }
+      if constexpr (SEG && FLAT) {
+        // the segment-start rows of this wave's 64 rows (below the tile's row count), in order,
+        // into half tid / 64 of the start list (the halves' counts come from smask)
+        const bool real = sstart && tid < M - m0;
+        const uint64_t rb = __ballot(real);
+        if (real) sd[BM + 2 + 16 + (tid & ~63) + __popcll(rb & ((1ull << (tid & 63)) - 1))] = tid;
+      }
     }
     if (BM == 64 && tid == 0) smask[2] = smask[3] = 0xffffffffu;  // rows 64.. (none): starts
   }
@@ -732,29 +743,69 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   if constexpr (TILE) {
     ep.template tile<BM, BN, NT, S::LDC, EP_IT, FLAT ? 0 : RPP>(pv, C, sd, m0, n0, tile, tid);
   } else {
-  // SEG: the tile's segment-start rows in order, then the row count (the segment pass's items);
-  // written here, read behind the barrier that ends the apply pass
-  int* slist = sd + BM + 2 + 16;
+  // SEG && FLAT: the tile's segment starts, written before the barrier above in two halves
+  // (rows 0..63 from slist[0], rows 64..127 from slist[64]); nh0 / nseg from the mask
+  const int* slist = sd + BM + 2 + 16;
   const int nrow_t = min(BM, M - m0);
   uint64_t mlo = 0, mhi = 0;
-  int nseg = 0;
+  int nseg = 0, nh0 = 0;
   if constexpr (SEG && FLAT) {
     mlo = smask[0] | ((uint64_t)smask[1] << 32);
     mhi = smask[2] | ((uint64_t)smask[3] << 32);
     // starts among rows < nrow_t (rows past the tile's count are sentinel starts)
     const uint64_t klo = nrow_t >= 64 ? mlo : mlo & ((1ull << nrow_t) - 1);
     const uint64_t khi = nrow_t >= 128 ? mhi : (nrow_t > 64 ? mhi & ((1ull << (nrow_t - 64)) - 1) : 0);
-    nseg = __popcll(klo) + __popcll(khi);
-    if (tid < nrow_t && seg_bit(mlo, mhi, tid)) {
-      const int below = tid < 64 ? __popcll(mlo & ((1ull << tid) - 1))
-                                 : __popcll(mlo) + __popcll(mhi & ((1ull << (tid - 64)) - 1));
-      slist[below] = tid;
-    }
-    if (tid == 0) slist[nseg] = nrow_t;
+    nh0 = __popcll(klo);
+    nseg = nh0 + __popcll(khi);
   }
+  auto seg_start = [&](int j) { return slist[j < nh0 ? j : 64 + (j - nh0)]; };
+  // segment [r, e) x column group c4 of the tile: a[v] stored, or handed over (crossing)
+  auto seg_out = [&](int r, int e, int c4, float4 a) {
+    if constexpr (SEG) {
+      const int col = n0 + 4 * c4;
+      const int v = sd[r + 1];
+      float* dst = ep.aout + (int64_t)v * ep.lda + col;
+      const bool head = r == 0 && sd[0] == v, tail = e == nrow_t && sd[nrow_t + 1] == v;
+      if (tail && !head && ep.znext)  // the tile where a crossing segment starts
+        *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + col) = f4zero();
+      if (head || tail) {
+        const int b = ep.dst_ptr[v], ee = ep.dst_ptr[v + 1];
+        if (seg_tiles(b, ee, BM) <= 2) {
+          atomicAdd(dst, a.x);
+          atomicAdd(dst + 1, a.y);
+          atomicAdd(dst + 2, a.z);
+          atomicAdd(dst + 3, a.w);
+        } else {
+          sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * c4, a);
+        }
+      } else {
+        st4_nt(dst, a);  // (common.hpp)
+      }
+    }
+  };
+  // SEG && FLAT && kB3SegMerge: ONE pass over (segment, column group) items -- each item applies
+  // its segment's rows in row order (h stored) and sums them: no h write-back to LDS, no second
+  // pass behind a barrier.  The lanes of a wave take consecutive column groups of one or two
+  // segments, so they run the same row count but at segment boundaries.
+  constexpr bool MERGE = SEG && FLAT && kB3SegMerge;
   auto apply_pass = [&](auto Ac) {
     constexpr int A = decltype(Ac)::value;
-    if constexpr (FLAT) {
+    if constexpr (MERGE) {
+#pragma unroll
+      for (int it = 0; it < EITF; ++it) {
+        const int q = tid + NT * it;
+        if (q >= nseg * C4) break;
+        const int j = q / C4, c4 = q - j * C4, col = n0 + 4 * c4;
+        if (col >= ep.N) continue;
+        const int r = seg_start(j), e = seg_end(mlo, mhi, r);
+        float4 a = f4zero();
+        for (int k = r; k < e; ++k)
+          a = f4add(a, ep.template apply4z_h<A>(
+                           m0 + k, col, *reinterpret_cast<const float4*>(&C[k * S::LDC + 4 * c4]),
+                           cx));
+        seg_out(r, e, c4, a);
+      }
+    } else if constexpr (FLAT) {
 #pragma unroll
       for (int it = 0; it < EP_IT; ++it) {
         const int q = tid + NT * it;
@@ -802,38 +853,18 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
     // partials onto zero: p + q == q + p, deterministic); one over three or more row tiles (a hub
     // node, in-degree > BM + 1) leaves its partial in a slot fixed by the data and its last
     // contributor sums the slots in row-tile order -- deterministic for every in-degree.
-    __syncthreads();
     const int nrow = nrow_t;
-    if constexpr (!FLAT) {
-      mlo = smask[0] | ((uint64_t)smask[1] << 32);
-      mhi = smask[2] | ((uint64_t)smask[3] << 32);
-    }
-    // segment [r, e) x column group c4
+    // segment [r, e) x column group c4 from the applied h rows in LDS
     auto seg_item = [&](int r, int e, int c4) {
-      const int col = n0 + 4 * c4;
-      const int v = sd[r + 1];
       float4 a = f4zero();
       for (int k = r; k < e; ++k)
         a = f4add(a, *reinterpret_cast<const float4*>(&C[k * S::LDC + 4 * c4]));
-      float* dst = ep.aout + (int64_t)v * ep.lda + col;
-      const bool head = r == 0 && sd[0] == v, tail = e == nrow && sd[nrow + 1] == v;
-      if (tail && !head && ep.znext)  // the tile where a crossing segment starts
-        *reinterpret_cast<float4*>(ep.znext + (int64_t)v * ep.lda + col) = f4zero();
-      if (head || tail) {
-        const int b = ep.dst_ptr[v], ee = ep.dst_ptr[v + 1];
-        if (seg_tiles(b, ee, BM) <= 2) {
-          atomicAdd(dst, a.x);
-          atomicAdd(dst + 1, a.y);
-          atomicAdd(dst + 2, a.z);
-          atomicAdd(dst + 3, a.w);
-        } else {
-          sc1_store4(ep.part + ((int64_t)tile * 2 + slot_of(tm, b / BM)) * BN + 4 * c4, a);
-        }
-      } else {
-        st4_nt(dst, a);  // (common.hpp)
-      }
+      seg_out(r, e, c4, a);
     };
-    if constexpr (FLAT) {
+    if constexpr (MERGE) {
+      // done by the apply pass
+    } else if constexpr (FLAT) {
+      __syncthreads();
       // items (segment j, column group c4) of the compact segment list: no lane waits on a
       // row that does not start a segment
 #pragma unroll
@@ -842,9 +873,13 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
         if (q >= nseg * C4) break;
         const int j = q / C4, c4 = q - j * C4;
         if (n0 + 4 * c4 >= ep.N) continue;
-        seg_item(slist[j], slist[j + 1], c4);
+        const int r = seg_start(j);
+        seg_item(r, seg_end(mlo, mhi, r), c4);
       }
     } else {
+      __syncthreads();
+      mlo = smask[0] | ((uint64_t)smask[1] << 32);
+      mhi = smask[2] | ((uint64_t)smask[3] << 32);
 #pragma unroll
       for (int it = 0; it < EIT; ++it) {
         const int r = er0 + RPP * it;
