@@ -20,7 +20,8 @@ Reference behaviours kept on purpose:
 Deliberate deviations: the readout's discarded ``lin`` output (``GNN.py:105``) is not
 computed; the scatter size is ``num_nodes`` instead of ``max(dst)+1`` (identical whenever the
 batch's last node has an incoming edge; ``CGR_STRICT=1`` raises like the reference otherwise);
-dropout masks come from a counter-based RNG seeded from torch's CPU generator, not ATen's.
+dropout masks come from a counter-based RNG keyed by the device's CUDA generator seed
+(``torch.cuda.default_generators``, what ``torch.manual_seed`` sets), not ATen's Philox stream.
 """
 
 from __future__ import annotations
