@@ -19,6 +19,9 @@ ABI_VERSION = 6
 TRAIN_DROPOUT, TRAIN_FOR_BACKWARD = 1, 2  # cgr_gnn_forward / _backward `training` bits
 MAX_DEPTH = 32
 ACT_RELU, ACT_SILU, ACT_GELU = 0, 1, 2
+ACT_TANH, ACT_SIGMOID, ACT_ELU, ACT_LEAKY_RELU, ACT_SOFTPLUS, ACT_MISH, ACT_SELU = 3, 4, 5, 6, 7, 8, 9
+ACT_NAMES = ("relu", "silu", "gelu", "tanh", "sigmoid", "elu", "leaky_relu", "softplus", "mish",
+             "selu")  # index = cgr_activation code (include/cgr_mpnn3d.h)
 
 
 class CgrGnnConfig(ctypes.Structure):

@@ -48,19 +48,32 @@ def _as(t, dtype, dev):
 
 
 def _activation_code(fn) -> int:
-    if fn is F.relu or fn is torch.relu:
-        return native.ACT_RELU
-    if fn is F.silu:
-        return native.ACT_SILU
-    if fn is F.gelu:
-        return native.ACT_GELU
-    name = getattr(fn, "__name__", "")
-    table = {"relu": native.ACT_RELU, "silu": native.ACT_SILU, "gelu": native.ACT_GELU}
-    if name in table:
-        return table[name]
+    """The native kernel code (``include/cgr_mpnn3d.h`` ``cgr_activation``) of ``activation_fn``.
+
+    The reference applies any callable (``GNN.py:86,127``); ``train.py:284-292`` offers F.relu /
+    F.silu / F.gelu.  Native kernels exist for those and for tanh, sigmoid, ELU, leaky_relu,
+    softplus, mish and SELU as functions (``F.*`` / ``torch.*``) or as ``nn`` modules at their
+    default parameters; anything else raises (there is no non-native path)."""
+    mods = {nn.ReLU: "relu", nn.SiLU: "silu", nn.GELU: "gelu", nn.Tanh: "tanh",
+            nn.Sigmoid: "sigmoid", nn.ELU: "elu", nn.LeakyReLU: "leaky_relu",
+            nn.Softplus: "softplus", nn.Mish: "mish", nn.SELU: "selu"}
+    name = None
+    if isinstance(fn, nn.Module):
+        name = mods.get(type(fn))
+        defaults = {"gelu": ("approximate", "none"), "elu": ("alpha", 1.0),
+                    "leaky_relu": ("negative_slope", 0.01), "softplus": ("beta", 1.0)}
+        if name in defaults and getattr(fn, defaults[name][0]) != defaults[name][1]:
+            name = None
+        if name == "softplus" and fn.threshold != 20.0:
+            name = None
+    else:
+        name = getattr(fn, "__name__", "")
+    if name in native.ACT_NAMES:
+        return native.ACT_NAMES.index(name)
     raise NotImplementedError(
-        f"cgr_mpnn_3D (MI355X): activation_fn {fn!r} has no native kernel; supported are "
-        "F.relu, F.silu, F.gelu (train.py:284-292)")
+        f"cgr_mpnn_3D (MI355X): activation_fn {fn!r} has no native kernel; supported are relu, "
+        "silu, gelu (train.py:284-292), tanh, sigmoid, elu, leaky_relu, softplus, mish, selu "
+        "(functions or default-parameter nn modules)")
 
 
 _UNPAIRED_MSG = (

@@ -348,7 +348,7 @@ static int validate_config(const cgr_gnn_config* c) {
   CGR_CHECK(c->num_edge_features >= 0, "cgr: num_edge_features must be >= 0");
   CGR_CHECK(c->hidden >= 1, "cgr: hidden size must be >= 1");
   CGR_CHECK(c->depth >= 1 && c->depth <= CGR_MAX_DEPTH, "cgr: depth must be in [1, 32]");
-  CGR_CHECK(c->activation >= 0 && c->activation <= 2, "cgr: unknown activation code");
+  CGR_CHECK(c->activation >= 0 && c->activation < ACT_COUNT, "cgr: unknown activation code");
   CGR_CHECK(c->aggregation == CGR_AGGR_ADD || c->aggregation == CGR_AGGR_MEAN,
             "cgr: unknown aggregation (CGR_AGGR_ADD, CGR_AGGR_MEAN)");
   CGR_CHECK(c->pooling == CGR_POOL_ADD || c->pooling == CGR_POOL_MEAN ||

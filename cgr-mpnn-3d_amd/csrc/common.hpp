@@ -24,25 +24,66 @@ __device__ __forceinline__ void st4_nt(float* p, const float4& v) {
   __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w}, reinterpret_cast<floatx4*>(p));
 }
 
-enum Act : int { ACT_RELU = 0, ACT_SILU = 1, ACT_GELU = 2 };
+// activation_fn of GNN.__init__ (reference GNN.py:21,127: any callable).  ReLU and SiLU have
+// kernels specialised at compile time; GELU and the rest share one runtime-selected slot (the
+// kernels' third instantiation, `A = -1`), with torch's default parameters: ELU alpha 1,
+// leaky_relu slope 0.01, softplus beta 1 / threshold 20, SELU's fixed constants.
+enum Act : int {
+  ACT_RELU = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_TANH = 3, ACT_SIGMOID = 4, ACT_ELU = 5,
+  ACT_LEAKY_RELU = 6, ACT_SOFTPLUS = 7, ACT_MISH = 8, ACT_SELU = 9, ACT_COUNT = 10
+};
+constexpr float kSeluAlpha = 1.6732632423543772848f, kSeluScale = 1.0507009873554804934f;
+
+__device__ __forceinline__ float softplus1(float z) { return z > 20.f ? z : log1pf(expf(z)); }
 
 __device__ __forceinline__ float act_fwd(float z, int act) {
   if (act == ACT_RELU) return z > 0.f ? z : 0.f;
   if (act == ACT_SILU) return z / (1.f + __expf(-z));
-  // GELU, exact erf form (F.gelu default approximate='none')
-  return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+  switch (act) {
+    case ACT_TANH: return tanhf(z);
+    case ACT_SIGMOID: return 1.f / (1.f + expf(-z));
+    case ACT_ELU: return z > 0.f ? z : expm1f(z);
+    case ACT_LEAKY_RELU: return z > 0.f ? z : 0.01f * z;
+    case ACT_SOFTPLUS: return softplus1(z);
+    case ACT_MISH: return z * tanhf(softplus1(z));
+    case ACT_SELU: return kSeluScale * (z > 0.f ? z : kSeluAlpha * expm1f(z));
+    default:  // GELU, exact erf form (F.gelu default approximate='none')
+      return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+  }
 }
 
-// d act / dz.  ReLU: 0 at z == 0 (ATen threshold_backward).
+// d act / dz.  ReLU: 0 at z == 0 (ATen threshold_backward); leaky_relu / ELU / SELU take the
+// negative branch at z == 0 as ATen's backward does (x > 0 ? 1 : ...).
 __device__ __forceinline__ float act_grad(float z, int act) {
   if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
   if (act == ACT_SILU) {
     const float s = 1.f / (1.f + __expf(-z));
     return s * (1.f + z * (1.f - s));
   }
-  const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
-  return cdf + z * pdf;
+  switch (act) {
+    case ACT_TANH: {
+      const float t = tanhf(z);
+      return 1.f - t * t;
+    }
+    case ACT_SIGMOID: {
+      const float s = 1.f / (1.f + expf(-z));
+      return s * (1.f - s);
+    }
+    case ACT_ELU: return z > 0.f ? 1.f : expf(z);
+    case ACT_LEAKY_RELU: return z > 0.f ? 1.f : 0.01f;
+    case ACT_SOFTPLUS: return z > 20.f ? 1.f : 1.f / (1.f + expf(-z));
+    case ACT_MISH: {
+      const float t = tanhf(softplus1(z));
+      const float s = 1.f / (1.f + expf(-z));
+      return t + z * s * (1.f - t * t);
+    }
+    case ACT_SELU: return z > 0.f ? kSeluScale : kSeluScale * kSeluAlpha * expf(z);
+    default: {
+      const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+      const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
+      return cdf + z * pdf;
+    }
+  }
 }
 
 // Counter-based dropout RNG: keep(seed, layer, element) is a pure function, so the backward

@@ -174,7 +174,7 @@ struct EpLayerBwdSeg {
     };
     if (a.act == ACT_RELU) rows(std::integral_constant<int, ACT_RELU>{});
     else if (a.act == ACT_SILU) rows(std::integral_constant<int, ACT_SILU>{});
-    else rows(std::integral_constant<int, ACT_GELU>{});
+    else rows(std::integral_constant<int, -1>{});  // GELU and the rest (common.hpp)
 
     CGR_STAMP(5);
     // ---- hand-off: the last contributor of a crossing segment (or of the grid) completes it ----

@@ -840,7 +840,7 @@ __global__ __launch_bounds__(WAVES * 64) void gemm_b3nt_kernel(AL al, const b3_u
   if constexpr (b3_ep_act<EP>::value) {  // one loop per activation, chosen once
     if (ep.act == ACT_RELU) apply_pass(std::integral_constant<int, ACT_RELU>{});
     else if (ep.act == ACT_SILU) apply_pass(std::integral_constant<int, ACT_SILU>{});
-    else apply_pass(std::integral_constant<int, ACT_GELU>{});
+    else apply_pass(std::integral_constant<int, -1>{});  // GELU and the rest
   } else {
     apply_pass(std::integral_constant<int, -1>{});
   }

@@ -299,7 +299,7 @@ int gnn_backward_impl(const Dims& d, const float* const* params, const cgr_batch
     else if (d.act == ACT_SILU)
       HIP_RET(launch_b3nt(LdActGradT<ACT_SILU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
     else
-      HIP_RET(launch_b3nt(LdActGradT<ACT_GELU>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
+      HIP_RET(launch_b3nt(LdActGradT<-1>{m, Hp, d.act}, img, rc, ep, N, H, H, st));
     return 0;
   };
   // capture order: fork, side work, then the main NT.  Enqueuing the NT first (the fork point

@@ -39,8 +39,13 @@ enum cgr_status {
   CGR_ERR_UNSUPPORTED = 3,
 };
 
-/* activation_fn of GNN.__init__ (GNN.py:21); train.py:284-292 offers F.relu / F.silu / F.gelu */
-enum cgr_activation { CGR_ACT_RELU = 0, CGR_ACT_SILU = 1, CGR_ACT_GELU = 2 };
+/* activation_fn of GNN.__init__ (GNN.py:21, applied at GNN.py:86,127: any callable); train.py:284-292
+ * offers F.relu / F.silu / F.gelu.  Codes 3-9 are further elementwise activations at torch's
+ * default parameters (ELU alpha 1, leaky_relu slope 0.01, softplus beta 1 / threshold 20). */
+enum cgr_activation {
+  CGR_ACT_RELU = 0, CGR_ACT_SILU = 1, CGR_ACT_GELU = 2, CGR_ACT_TANH = 3, CGR_ACT_SIGMOID = 4,
+  CGR_ACT_ELU = 5, CGR_ACT_LEAKY_RELU = 6, CGR_ACT_SOFTPLUS = 7, CGR_ACT_MISH = 8, CGR_ACT_SELU = 9
+};
 
 /* GNN.__init__(num_node_features, num_edge_features, depth, hidden_sizes, dropout_ps,
  *              activation_fn, aggr="add", pooling_fn=global_add_pool, use_learnable_skip)

@@ -35,7 +35,9 @@ except Exception:  # pragma: no cover
     _sp = None
     _erf = None
 
-ACT_CODES = {"relu": 0, "silu": 1, "gelu": 2}
+ACT_CODES = {"relu": 0, "silu": 1, "gelu": 2, "tanh": 3, "sigmoid": 4, "elu": 5, "leaky_relu": 6,
+             "softplus": 7, "mish": 8, "selu": 9}
+_SELU_ALPHA, _SELU_SCALE = 1.6732632423543772848170429916717, 1.0507009873554804934193349852946
 
 
 # ----------------------------------------------------------------------------------------------
@@ -48,6 +50,21 @@ def act_fwd(z: np.ndarray, act: str) -> np.ndarray:
         return z / (1.0 + np.exp(-z))
     if act == "gelu":
         return 0.5 * z * (1.0 + _erf(z / np.sqrt(2.0)))
+    # further elementwise activations at torch's default parameters (torch.nn.functional)
+    if act == "tanh":
+        return np.tanh(z)
+    if act == "sigmoid":
+        return 1.0 / (1.0 + np.exp(-z))
+    if act == "elu":
+        return np.where(z > 0, z, np.expm1(np.minimum(z, 0.0)))
+    if act == "leaky_relu":
+        return np.where(z > 0, z, 0.01 * z)
+    if act == "softplus":
+        return np.where(z > 20.0, z, np.log1p(np.exp(np.minimum(z, 20.0))))
+    if act == "mish":
+        return z * np.tanh(act_fwd(z, "softplus"))
+    if act == "selu":
+        return _SELU_SCALE * np.where(z > 0, z, _SELU_ALPHA * np.expm1(np.minimum(z, 0.0)))
     raise ValueError(act)
 
 
@@ -62,6 +79,23 @@ def act_grad(z: np.ndarray, act: str) -> np.ndarray:
         cdf = 0.5 * (1.0 + _erf(z / np.sqrt(2.0)))
         pdf = np.exp(-0.5 * z * z) / np.sqrt(2.0 * np.pi)
         return cdf + z * pdf
+    if act == "tanh":
+        return 1.0 - np.tanh(z) ** 2
+    if act == "sigmoid":
+        s = 1.0 / (1.0 + np.exp(-z))
+        return s * (1.0 - s)
+    if act == "elu":  # ATen elu_backward: x > 0 ? 1 : alpha * exp(x)
+        return np.where(z > 0, 1.0, np.exp(np.minimum(z, 0.0)))
+    if act == "leaky_relu":
+        return np.where(z > 0, 1.0, 0.01).astype(z.dtype)
+    if act == "softplus":
+        return np.where(z > 20.0, 1.0, 1.0 / (1.0 + np.exp(-z)))
+    if act == "mish":
+        t = np.tanh(act_fwd(z, "softplus"))
+        s = 1.0 / (1.0 + np.exp(-z))
+        return t + z * s * (1.0 - t * t)
+    if act == "selu":
+        return _SELU_SCALE * np.where(z > 0, 1.0, _SELU_ALPHA * np.exp(np.minimum(z, 0.0)))
     raise ValueError(act)
 
 

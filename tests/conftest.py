@@ -14,6 +14,19 @@ for p in (REPO, PKG):
 
 GOLDEN_DIR = os.path.join(REPO, "tests", "golden")
 
+# activation name -> the callable handed to GNN(activation_fn=...); the order is the native
+# cgr_activation code (include/cgr_mpnn3d.h)
+ACT_NAMES = ("relu", "silu", "gelu", "tanh", "sigmoid", "elu", "leaky_relu", "softplus", "mish",
+             "selu")
+
+
+def act_fn(name):
+    import torch
+    import torch.nn.functional as F
+    return {"relu": F.relu, "silu": F.silu, "gelu": F.gelu, "tanh": torch.tanh,
+            "sigmoid": torch.sigmoid, "elu": F.elu, "leaky_relu": F.leaky_relu,
+            "softplus": F.softplus, "mish": F.mish, "selu": F.selu}[name]
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")

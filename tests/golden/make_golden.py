@@ -118,7 +118,9 @@ class _Data:
         self.x, self.edge_index, self.edge_attr, self.batch = x, edge_index, edge_attr, batch
 
 
-ACTS = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu}
+ACTS = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu, "tanh": torch.tanh, "sigmoid": torch.sigmoid,
+        "elu": F.elu, "leaky_relu": F.leaky_relu, "softplus": F.softplus, "mish": F.mish,
+        "selu": F.selu}
 
 # name -> (batch kwargs, model kwargs, extra)
 CASES = {
@@ -174,6 +176,15 @@ CASES = {
                            dict(depth=2, hidden=24, act="gelu", skip=False),
                            {"pool": "max", "batch_none": True}),
 }
+# activation_fn beyond train.py's three (the reference applies any callable, GNN.py:86,127): one
+# small ragged case per further activation, alternating skip / aggregation / pooling
+for _i, (_act, _skip, _ex) in enumerate([("tanh", True, {}), ("sigmoid", False, {"aggr": "mean"}),
+                                         ("elu", True, {}), ("leaky_relu", False, {}),
+                                         ("softplus", True, {"pool": "mean"}),
+                                         ("mish", False, {}), ("selu", True, {})]):
+    CASES[f"act_{_act}"] = (dict(num_graphs=3, n_atoms=12, n_bonds=13, n_mace=8, seed=40 + _i,
+                                 n_atoms_jitter=4),
+                            dict(depth=2, hidden=24, act=_act, skip=_skip), _ex)
 
 
 def run_case(ref, name, bkw, mkw, extra):

@@ -84,7 +84,7 @@ def test_arena_and_workspace_sizes_scale():
     assert lib.cgr_gnn_arena_offset(ctypes.byref(c_silu), 7680, 15360, 256, b"pre", 1) > 0
 
 
-@pytest.mark.parametrize("bad", [dict(D=0), dict(D=33), dict(H=0), dict(act=7), dict(Fe=-1)])
+@pytest.mark.parametrize("bad", [dict(D=0), dict(D=33), dict(H=0), dict(act=10), dict(act=-1), dict(Fe=-1)])
 def test_invalid_config_is_rejected_with_message(bad):
     lib = native.load()
     c = _cfg(**bad)

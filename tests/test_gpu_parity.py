@@ -13,7 +13,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import golden_cases, load_golden
+from conftest import ACT_NAMES, act_fn, golden_cases, load_golden
 
 from cgr_mpnn_3D._amd import native
 from cgr_mpnn_3D._amd.debug import ArenaRun
@@ -24,7 +24,7 @@ from oracle import dmpnn_numpy as on
 
 pytestmark = pytest.mark.gpu
 
-ACT = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu}
+ACT = {n: act_fn(n) for n in ACT_NAMES}
 Y_RTOL = 1e-4
 G_RTOL = 1e-4
 
@@ -191,7 +191,8 @@ def test_cfg2_input_gradients_vs_oracle(cuda_device):
     _oracle_compare(make_batch(32, seed=23), 400, 4, "relu", False, cuda_device, inputs=True)
 
 
-@pytest.mark.parametrize("H,act", [(21, "silu"), (18, "gelu"), (64, "relu")])
+@pytest.mark.parametrize("H,act", [(21, "silu"), (18, "gelu"), (64, "relu"), (22, "tanh"),
+                                   (40, "mish")])
 def test_input_gradients_odd_widths_vs_oracle(H, act, cuda_device):
     # H % 4 != 0: the [Gs | dzn] concat loader's narrower vector widths; x of F = 78 (padded rows)
     b = make_batch(6, n_atoms=14, n_bonds=16, n_mace=0, seed=31, n_atoms_jitter=5)
@@ -210,7 +211,7 @@ def test_edge_feature_widths_vs_oracle(Fe, cuda_device):
 
 
 def _cfg_tuple(F_, Fe, H, D, act, skip, aggr="add", pool="add"):
-    return (F_, Fe, H, D, {"relu": 0, "silu": 1, "gelu": 2}[act], skip,
+    return (F_, Fe, H, D, ACT_NAMES.index(act), skip,
             {"add": 0, "mean": 1}[aggr], {"add": 0, "mean": 1, "max": 2}[pool])
 
 
@@ -464,7 +465,8 @@ def test_cfg2_eight_shard_gradients_sum_to_whole_batch(cuda_device):
         assert_g_close(gsum[k].cpu().numpy(), g_all[k].cpu().numpy(), k)
 
 
-@pytest.mark.parametrize("act", ["silu", "gelu"])
+@pytest.mark.parametrize("act", ["silu", "gelu", "tanh", "sigmoid", "elu", "leaky_relu",
+                                 "softplus", "mish", "selu"])
 def test_smooth_activations_vs_oracle(act, cuda_device):
     _oracle_compare(make_batch(12, n_atoms=30, n_bonds=34, n_mace=40, seed=23), 128, 3, act, True,
                     cuda_device)

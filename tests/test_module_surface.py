@@ -5,7 +5,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import golden_cases, load_golden
+from conftest import act_fn, golden_cases, load_golden
 
 from cgr_mpnn_3D.models.GNN import GNN, DMPNNConv, global_add_pool
 
@@ -17,7 +17,7 @@ def test_state_dict_keys_shapes_and_seeded_init_match_reference(case):
     torch.manual_seed(1000 + len(case))  # the seed make_golden.py used before ref.GNN(...)
     m = GNN(meta["num_node_features"], meta["num_edge_features"], depth=D, hidden_sizes=[H] * D,
             dropout_ps=[meta["eval_dropout"]] * D,
-            activation_fn={"relu": F.relu, "silu": F.silu, "gelu": F.gelu}[meta["act"]],
+            activation_fn=act_fn(meta["act"]),
             use_learnable_skip=meta["skip"])
     sd = m.state_dict()
     ref_keys = [k[2:] for k in z.files if k.startswith("p_")]

@@ -5,11 +5,11 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from conftest import golden_cases, load_golden
+from conftest import ACT_NAMES, act_fn, golden_cases, load_golden
 from oracle import dmpnn_numpy as on
 from oracle.dmpnn_torch import TorchRestatement, random_state_dict
 
-ACT = {"relu": F.relu, "silu": F.silu, "gelu": F.gelu}
+ACT = {n: act_fn(n) for n in ACT_NAMES}
 CASES = golden_cases()
 
 
@@ -53,8 +53,12 @@ def test_numpy_oracle_gradients_match_reference(case):
     assert abs(loss - float(z["out_loss"])) <= 1e-5 * abs(float(z["out_loss"]))
     ref_keys = {k[2:] for k in z.files if k.startswith("g_")}
     assert set(grads) == ref_keys
+    # the goldens are the reference's fp32 autograd, the oracle is fp64: the bar is the reference's
+    # own rounding.  Under sigmoid (derivative <= 1/4, saturating) the layer weight gradients are
+    # small sums of larger fp32 terms, and the reference's relative error reaches 1.4e-5
+    tol = 3e-5 if meta["act"] == "sigmoid" else 1e-5
     for k in ref_keys:
-        assert rel_err(grads[k], z["g_" + k]) < 1e-5, k
+        assert rel_err(grads[k], z["g_" + k]) < tol, k
 
 
 @pytest.mark.parametrize("case", CASES)
