@@ -36,9 +36,9 @@ constexpr float kSeluAlpha = 1.6732632423543772848f, kSeluScale = 1.050700987355
 
 __device__ __forceinline__ float softplus1(float z) { return z > 20.f ? z : log1pf(expf(z)); }
 
-__device__ __forceinline__ float act_fwd(float z, int act) {
-  if (act == ACT_RELU) return z > 0.f ? z : 0.f;
-  if (act == ACT_SILU) return z / (1.f + __expf(-z));
+// codes 3-9: out of line, so the fused kernels that carry the runtime slot keep GELU's register
+// budget and code size (inlined, the switch grew the fused layer backward by 13 us per launch)
+__device__ __attribute__((noinline)) static float act_fwd_ext(float z, int act) {
   switch (act) {
     case ACT_TANH: return tanhf(z);
     case ACT_SIGMOID: return 1.f / (1.f + expf(-z));
@@ -46,20 +46,12 @@ __device__ __forceinline__ float act_fwd(float z, int act) {
     case ACT_LEAKY_RELU: return z > 0.f ? z : 0.01f * z;
     case ACT_SOFTPLUS: return softplus1(z);
     case ACT_MISH: return z * tanhf(softplus1(z));
-    case ACT_SELU: return kSeluScale * (z > 0.f ? z : kSeluAlpha * expm1f(z));
-    default:  // GELU, exact erf form (F.gelu default approximate='none')
-      return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+    default: return kSeluScale * (z > 0.f ? z : kSeluAlpha * expm1f(z));  // ACT_SELU
   }
 }
 
-// d act / dz.  ReLU: 0 at z == 0 (ATen threshold_backward); leaky_relu / ELU / SELU take the
-// negative branch at z == 0 as ATen's backward does (x > 0 ? 1 : ...).
-__device__ __forceinline__ float act_grad(float z, int act) {
-  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
-  if (act == ACT_SILU) {
-    const float s = 1.f / (1.f + __expf(-z));
-    return s * (1.f + z * (1.f - s));
-  }
+// leaky_relu / ELU / SELU take the negative branch at z == 0 as ATen's backward does
+__device__ __attribute__((noinline)) static float act_grad_ext(float z, int act) {
   switch (act) {
     case ACT_TANH: {
       const float t = tanhf(z);
@@ -77,13 +69,31 @@ __device__ __forceinline__ float act_grad(float z, int act) {
       const float s = 1.f / (1.f + expf(-z));
       return t + z * s * (1.f - t * t);
     }
-    case ACT_SELU: return z > 0.f ? kSeluScale : kSeluScale * kSeluAlpha * expf(z);
-    default: {
-      const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
-      const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
-      return cdf + z * pdf;
-    }
+    default: return z > 0.f ? kSeluScale : kSeluScale * kSeluAlpha * expf(z);  // ACT_SELU
   }
+}
+
+__device__ __forceinline__ float act_fwd(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? z : 0.f;
+  if (act == ACT_SILU) return z / (1.f + __expf(-z));
+  // GELU, exact erf form (F.gelu default approximate='none')
+  if (act == ACT_GELU) return 0.5f * z * (1.f + erff(z * 0.70710678118654752f));
+  return act_fwd_ext(z, act);
+}
+
+// d act / dz.  ReLU: 0 at z == 0 (ATen threshold_backward).
+__device__ __forceinline__ float act_grad(float z, int act) {
+  if (act == ACT_RELU) return z > 0.f ? 1.f : 0.f;
+  if (act == ACT_SILU) {
+    const float s = 1.f / (1.f + __expf(-z));
+    return s * (1.f + z * (1.f - s));
+  }
+  if (act == ACT_GELU) {
+    const float cdf = 0.5f * (1.f + erff(z * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * __expf(-0.5f * z * z);
+    return cdf + z * pdf;
+  }
+  return act_grad_ext(z, act);
 }
 
 // Counter-based dropout RNG: keep(seed, layer, element) is a pure function, so the backward
