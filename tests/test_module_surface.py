@@ -88,3 +88,24 @@ def test_unpickling_a_reference_style_module_fills_native_state(tmp_path):
     assert m2._grad_bucket_hook is None
     assert "_cgr_rng_counter" in m2._buffers and isinstance(m2._cgr_instance, int)
     assert set(m2.state_dict()) == set(m.state_dict())
+
+
+def test_activation_codes_cover_functions_and_default_modules():
+    # the native cgr_activation code per activation_fn (GNN.py:86,127 applies any callable);
+    # non-default module parameters and other callables raise: there is no non-native path
+    import torch.nn as nn
+    from cgr_mpnn_3D._amd import native
+    from cgr_mpnn_3D.models.GNN import _activation_code
+    fns = {"relu": (F.relu, torch.relu, nn.ReLU()), "silu": (F.silu, nn.SiLU()),
+           "gelu": (F.gelu, nn.GELU()), "tanh": (torch.tanh, F.tanh, nn.Tanh()),
+           "sigmoid": (torch.sigmoid, F.sigmoid, nn.Sigmoid()), "elu": (F.elu, nn.ELU()),
+           "leaky_relu": (F.leaky_relu, nn.LeakyReLU()), "softplus": (F.softplus, nn.Softplus()),
+           "mish": (F.mish, nn.Mish()), "selu": (F.selu, torch.selu, nn.SELU())}
+    assert set(fns) == set(native.ACT_NAMES)
+    for name, cands in fns.items():
+        for fn in cands:
+            assert _activation_code(fn) == native.ACT_NAMES.index(name), (name, fn)
+    for bad in (nn.GELU(approximate="tanh"), nn.LeakyReLU(0.2), nn.ELU(alpha=0.5),
+                nn.Softplus(beta=2.0), nn.Softplus(threshold=10.0), torch.abs, lambda t: t):
+        with pytest.raises(NotImplementedError):
+            _activation_code(bad)
